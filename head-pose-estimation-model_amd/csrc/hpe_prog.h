@@ -1,0 +1,56 @@
+// hpe_prog.h — word layout of a compiled "row program" (shared by hpe/compiler.py and the kernels).
+//
+// A head model of the reference (every builder in Model-96/train_96.py:65-110,
+// Model-88/train_88.py:66-253, Model-88/attention_model.py:16-169 and all 684 checkpoint graphs) is,
+// per spatial position, a DAG of 1x1-conv / dense GEMMs, element-wise epilogues and row-local
+// normalisations.  The compiler lowers it to a flat op list that one persistent HIP kernel
+// interprets over tiles of T rows held in LDS: activations never leave the CU, only the input
+// rows stream from HBM.
+#pragma once
+
+#define HPE_MAGIC 0x31455048  // "HPE1"
+
+// ---- header words ------------------------------------------------------------------------------
+enum {
+  H_MAGIC = 0, H_NOPS, H_NSLOTS, H_T, H_NW, H_IN_SLOT, H_OUT_SLOT, H_CIN, H_COUT,
+  H_NPARAMS, H_NPARAMS_TRAIN, H_LDS_FLOATS, H_MAXACC, H_MAXTHIN, H_NTACC, H_OPS_OFF,
+  H_SLOTS_OFF, H_BLK_OFF, H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB,
+  H_WORDS = 32
+};
+
+enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_EVAL = 2 };
+
+// ---- slot words: LDS float offset, channels, padded channels (even, %8), row stride -----------
+enum { S_OFF = 0, S_C, S_CP, S_STRIDE, S_WORDS = 4 };
+
+// ---- op words -----------------------------------------------------------------------------------
+enum {
+  O_TYPE = 0, O_A, O_B, O_OUT, O_K, O_N, O_W, O_BIAS, O_FLAGS,
+  O_EACT, O_EDROP, O_ETHR, O_EKEEP, O_EZ,   // epilogue: activation, dropout ordinal/threshold/keep-prob, z slot
+  O_AUX0, O_AUX1, O_AUX2, O_AUX3, O_TBASE, O_TCOUNT, O_F0, O_F1, O_MODE, O_WSEL,
+  O_WORDS = 24
+};
+
+enum {
+  OP_DENSE = 1,    // out = epi(a . W + b)                       MFMA 32x32x2 f32
+  OP_TDENSE = 2,   // same, N <= 8, VALU with K split over threads
+  OP_EW = 3,       // out = epi((f0 a + f1 b | a * b) * s + t)
+  OP_LN = 4,       // out = epi(LayerNorm(a))  (+ xhat / rstd for backward)
+  OP_LOSS = 5,     // MSE/MAE partial sums; out = dL/dpred through the producer's epilogue
+  OP_EPIGRAD = 6,  // out <- out * epi'(a)                       (in place)
+  OP_DW = 7,       // dW blocks += a^T . b                       MFMA, register accumulators
+  OP_TACC = 8,     // thin per-thread accumulators (small dW, bias, per-channel scale grads)
+  OP_DIN = 9,      // out (=|+=|epigrad) a . W^T                 MFMA
+  OP_TDIN = 10,    // same, contraction N <= 8, VALU
+  OP_EWB = 11,     // backward of OP_EW
+  OP_LNB = 12      // backward of OP_LN
+};
+
+enum { EW_HAS_B = 1, EW_MUL = 2, EW_AFFINE = 4 };             // OP_EW / OP_EWB flags
+enum { DST_STORE = 0, DST_ACCUM = 1, DST_EPIGRAD = 2 };       // O_MODE of DIN/TDIN/EWB/LNB
+enum { TACC_GEMM = 0, TACC_BIAS = 1, TACC_DIAG = 2 };         // O_AUX3 of OP_TACC
+
+enum {
+  ACT_LINEAR = 0, ACT_TANH, ACT_RELU, ACT_SOFTSIGN, ACT_SIGMOID, ACT_ELU, ACT_SELU, ACT_SWISH,
+  ACT_SOFTPLUS, ACT_LEAKY_RELU
+};

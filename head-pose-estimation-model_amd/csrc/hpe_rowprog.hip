@@ -1,0 +1,1027 @@
+// hpe_rowprog.hip — the head-pose regression hot path on MI355X (gfx950 / CDNA4).
+//
+// One persistent kernel interprets a compiled row program (hpe_prog.h) over tiles of T rows
+// (positions of the NHWC feature maps, channels-last).  Per tile:
+//   * the input rows (T x C_in fp32, contiguous in HBM) are loaded once, coalesced, into LDS;
+//   * every 1x1-conv / dense layer runs as fp32 MFMA (v_mfma_f32_32x32x2_f32: exact f32, the
+//     reference's fp32 numerics) with A = activations from LDS (ds_read_b128 along K, rows on the
+//     lanes, conflict-free row stride) and B = weights from L2 (coalesced 128-B rows);
+//   * bias + activation + SpatialDropout are fused into the GEMM epilogue, results go back to LDS;
+//   * in training, the loss gradient, every backward GEMM and element-wise backward run on the
+//     same LDS tile, and the weight gradients accumulate in MFMA accumulators that stay in
+//     registers for the whole launch (each wave owns fixed 32x32 dW blocks); thin layers (N <= 8,
+//     e.g. the 3-channel yaw/pitch/roll head) run on the VALU.
+// HBM traffic is therefore the compulsory input read (+ 12 B/row output in inference) — the
+// intermediate activations of the reference's Keras graph never leave the CU.
+//
+// Reference semantics restated: Conv2D/Dense + activation (train_96.py:72-92), SpatialDropout2D
+// (train_96.py:82,94), Add/Average/Multiply/Activation (attention_model.py:38,56,60,148-149),
+// LayerNormalization (attention_model.py:57,61), MSE loss + MAE metric (train_96.py:51-52), the
+// autodiff of Keras' fit (train_96.py:175).  Optimizers: Keras legacy SGD/Adam/Adamax.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "hpe_prog.h"
+#include "../../include/hpe.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MAXTHIN 4
+
+// ------------------------------------------------------------------------------------------------
+// activations and their derivatives (derivative from the stored output where possible)
+// ------------------------------------------------------------------------------------------------
+#define SELU_ALPHA 1.6732632423543772848170429916717f
+#define SELU_SCALE 1.0507009873554804934193349852946f
+
+__device__ __forceinline__ float act_f(int act, float z) {
+  switch (act) {
+    case ACT_TANH: return tanhf(z);
+    case ACT_RELU: return z > 0.f ? z : 0.f;
+    case ACT_SOFTSIGN: return z / (1.f + fabsf(z));
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-z));
+    case ACT_ELU: return z > 0.f ? z : expm1f(z);
+    case ACT_SELU: return SELU_SCALE * (z > 0.f ? z : SELU_ALPHA * expm1f(z));
+    case ACT_SWISH: return z / (1.f + expf(-z));
+    case ACT_SOFTPLUS: return z > 20.f ? z : log1pf(expf(z));
+    case ACT_LEAKY_RELU: return z > 0.f ? z : 0.2f * z;
+    default: return z;
+  }
+}
+
+// d act / dz given a = act(z) (and z for swish)
+__device__ __forceinline__ float act_grad(int act, float a, float z) {
+  switch (act) {
+    case ACT_TANH: return 1.f - a * a;
+    case ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case ACT_SOFTSIGN: { float t = 1.f - fabsf(a); return t * t; }
+    case ACT_SIGMOID: return a * (1.f - a);
+    case ACT_ELU: return a > 0.f ? 1.f : a + 1.f;
+    case ACT_SELU: return a > 0.f ? SELU_SCALE : a + SELU_SCALE * SELU_ALPHA;
+    case ACT_SWISH: { float s = 1.f / (1.f + expf(-z)); return s * (1.f + z * (1.f - s)); }
+    case ACT_SOFTPLUS: return -expm1f(-a);
+    case ACT_LEAKY_RELU: return a > 0.f ? 1.f : 0.2f;
+    default: return 1.f;
+  }
+}
+
+// SpatialDropout2D keep test: counter hash of (seed, dropout ordinal, image, channel).
+// Restated bit-for-bit by oracle/keras_ref.py:dropout_hash.
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int drop_id, uint64_t image, uint32_t c) {
+  uint64_t x = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(1 + drop_id);
+  x ^= image * 0xBF58476D1CE4E5B9ull;
+  x ^= (uint64_t)c * 0xD6E8FEB86659FD93ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+
+struct Epi {
+  int act, drop, zslot;
+  uint32_t thr;
+  float keep;
+};
+
+struct Ctx {
+  const int* prog;
+  const float* params;
+  const float* params_t;
+  float* lds;
+  int T;
+  int64_t row0;     // first row of the tile (batch-local)
+  int64_t nrows;    // valid rows
+  int P;            // positions per image
+  int64_t img_off;  // global index of this launch's first image (dropout hash)
+  uint64_t seed;
+};
+
+__device__ __forceinline__ int slot_w(const Ctx& c, int s, int w) {
+  return c.prog[c.prog[H_SLOTS_OFF] + s * S_WORDS + w];
+}
+
+__device__ __forceinline__ Epi load_epi(const int* o) {
+  Epi e;
+  e.act = o[O_EACT];
+  e.drop = o[O_EDROP];
+  e.zslot = o[O_EZ];
+  e.thr = (uint32_t)o[O_ETHR];
+  e.keep = __int_as_float(o[O_EKEEP]);
+  return e;
+}
+
+__device__ __forceinline__ int64_t image_of(const Ctx& c, int r) {
+  return (c.row0 + r) / c.P + c.img_off;
+}
+
+__device__ __forceinline__ float epi_fwd(const Ctx& c, const Epi& e, float z, int r, int ch) {
+  float a = act_f(e.act, z);
+  if (e.drop >= 0) a = drop_hash(c.seed, e.drop, image_of(c, r), ch) >= e.thr ? a / e.keep : 0.f;
+  return a;
+}
+
+// gradient through the epilogue: g = dL/d(stored output), val = stored output
+__device__ __forceinline__ float epi_bwd(const Ctx& c, const Epi& e, float g, float val, float z,
+                                         int r, int ch) {
+  if (e.drop >= 0) {
+    if (drop_hash(c.seed, e.drop, image_of(c, r), ch) < e.thr) return 0.f;
+    g = g / e.keep;
+    val = val * e.keep;
+  }
+  return e.act == ACT_LINEAR ? g : g * act_grad(e.act, val, z);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_DENSE: out[r][n] = epi(sum_k a[r][k] W[k][n] + b[n]) on fp32 MFMA 32x32x2.
+// A[i=row][k] from LDS; contraction split across the lane halves: half h handles k in
+// [h*Kh, h*Kh + Kh) (Kh = Cp/2, a multiple of 4) so each lane reads 4 consecutive k with one
+// ds_read_b128; slot stride = 4*odd floats makes the 16-row lane groups conflict-free.
+// B[k][j=n] = W[k][n]: lanes 0-31 / 32-63 read one contiguous 128-B W row each (L2-resident).
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_dense(const Ctx& c, const int* o) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int sa = o[O_A], so = o[O_OUT];
+  const int a_off = slot_w(c, sa, S_OFF), a_cp = slot_w(c, sa, S_CP), a_st = slot_w(c, sa, S_STRIDE);
+  const int o_off = slot_w(c, so, S_OFF), o_st = slot_w(c, so, S_STRIDE), o_cp = slot_w(c, so, S_CP);
+  const int K = o[O_K], N = o[O_N];
+  const float* W = (o[O_WSEL] ? c.params_t : c.params) + o[O_W];
+  const int boff = o[O_BIAS];
+  const Epi e = load_epi(o);
+  const int nrb = c.T >> 5, ncb = (N + 31) >> 5;
+  const int Kh = a_cp >> 1;
+  const int kbase = half * Kh;
+  const int kval = K - kbase;  // valid k count for this half
+  for (int task = wave; task < nrb * ncb; task += NW) {
+    const int cb = task / nrb, rb = task - cb * nrb;
+    const int n = cb * 32 + l32;
+    const bool nok = n < N;
+    const float* ap = c.lds + a_off + (rb * 32 + l32) * a_st + kbase;
+    const float* bp = W + (size_t)kbase * N + (nok ? n : 0);
+    f32x16 acc = {};
+    int m = 0;
+    for (; m + 8 <= Kh; m += 8) {
+      const f32x4 a0 = *(const f32x4*)(ap + m);
+      const f32x4 a1 = *(const f32x4*)(ap + m + 4);
+      float b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = (nok && m + j < kval) ? bp[(size_t)(m + j) * N] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b[3], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b[4], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b[5], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, b[6], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, b[7], acc, 0, 0, 0);
+    }
+    for (; m < Kh; m += 4) {
+      const f32x4 a0 = *(const f32x4*)(ap + m);
+      float b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (nok && m + j < kval) ? bp[(size_t)(m + j) * N] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b[3], acc, 0, 0, 0);
+    }
+    if (nok) {
+      const float bv = boff >= 0 ? c.params[boff + n] : 0.f;
+      const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0;
+      const int z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int r = rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        const float z = acc[g] + bv;
+        c.lds[o_off + r * o_st + n] = epi_fwd(c, e, z, r, n);
+        if (e.zslot >= 0) c.lds[z_off + r * z_st + n] = z;
+      }
+    } else if (n < o_cp) {  // keep the K-padding columns of the output slot zero (LDS reuse)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c.lds[o_off + (rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * o_st + n] = 0.f;
+    }
+  }
+}
+
+// zero the padding columns [C, Cp) of a slot just (re)defined: slots share LDS over the op list,
+// and the MFMA A-operand reads of OP_DENSE / OP_DIN cover Cp columns
+template <int NW>
+__device__ __forceinline__ void zero_pads(const Ctx& c, int slot, int C) {
+  constexpr int NT = NW * 64;
+  const int cp = slot_w(c, slot, S_CP);
+  const int np = cp - C;
+  if (np <= 0) return;
+  const int off = slot_w(c, slot, S_OFF), st = slot_w(c, slot, S_STRIDE);
+  for (int it = threadIdx.x; it < c.T * np; it += NT) {
+    const int r = it / np, j = it - r * np;
+    c.lds[off + r * st + C + j] = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_TDENSE: thin layer (N <= 8, e.g. the 3-channel pose head) on the VALU; K split S ways over
+// threads, partials through LDS scratch, summed in fixed order (deterministic).
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_tdense(const Ctx& c, const int* o) {
+  constexpr int NT = NW * 64;
+  const int sa = o[O_A], so = o[O_OUT];
+  const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
+  const int o_off = slot_w(c, so, S_OFF), o_st = slot_w(c, so, S_STRIDE);
+  const int K = o[O_K], N = o[O_N], S = o[O_AUX3];
+  const float* W = (o[O_WSEL] ? c.params_t : c.params) + o[O_W];
+  const int boff = o[O_BIAS];
+  const Epi e = load_epi(o);
+  float* scratch = c.lds + o[O_AUX2];  // per-op transient region (liveness-planned)
+  const int TN = c.T * N;
+  const int kc = (K + S - 1) / S;
+  for (int it = threadIdx.x; it < TN * S; it += NT) {
+    const int s = it / TN, rn = it - s * TN;
+    const int r = rn / N, n = rn - r * N;
+    const int k0 = s * kc, k1 = min(K, k0 + kc);
+    const float* ap = c.lds + a_off + r * a_st;
+    float acc = 0.f;
+    for (int k = k0; k < k1; ++k) acc = fmaf(ap[k], W[k * N + n], acc);
+    scratch[it] = acc;
+  }
+  __syncthreads();
+  for (int rn = threadIdx.x; rn < TN; rn += NT) {
+    const int r = rn / N, n = rn - r * N;
+    float z = 0.f;
+    for (int s = 0; s < S; ++s) z += scratch[s * TN + rn];
+    if (boff >= 0) z += c.params[boff + n];
+    c.lds[o_off + r * o_st + n] = epi_fwd(c, e, z, r, n);
+    if (e.zslot >= 0) c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + n] = z;
+  }
+  zero_pads<NW>(c, so, N);
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_EW: element-wise (Add / Average / Multiply / Activation / BatchNorm-affine / depthwise-1x1
+// scale / standalone SpatialDropout) with the fused epilogue.
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_ew(const Ctx& c, const int* o) {
+  constexpr int NT = NW * 64;
+  const int flags = o[O_FLAGS];
+  const int C = slot_w(c, o[O_OUT], S_C);
+  const int a_off = slot_w(c, o[O_A], S_OFF), a_st = slot_w(c, o[O_A], S_STRIDE);
+  const int b_off = (flags & EW_HAS_B) ? slot_w(c, o[O_B], S_OFF) : 0;
+  const int b_st = (flags & EW_HAS_B) ? slot_w(c, o[O_B], S_STRIDE) : 0;
+  const int o_off = slot_w(c, o[O_OUT], S_OFF), o_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const float f0 = __int_as_float(o[O_F0]), f1 = __int_as_float(o[O_F1]);
+  const int soff = o[O_AUX0], toff = o[O_AUX1];
+  const Epi e = load_epi(o);
+  for (int it = threadIdx.x; it < c.T * C; it += NT) {
+    const int r = it / C, ch = it - r * C;
+    const float va = c.lds[a_off + r * a_st + ch];
+    float v;
+    if (flags & EW_MUL) v = va * c.lds[b_off + r * b_st + ch];
+    else v = (flags & EW_HAS_B) ? f0 * va + f1 * c.lds[b_off + r * b_st + ch] : f0 * va;
+    if (flags & EW_AFFINE) v = v * c.params[soff + ch] + (toff >= 0 ? c.params[toff + ch] : 0.f);
+    c.lds[o_off + r * o_st + ch] = epi_fwd(c, e, v, r, ch);
+    if (e.zslot >= 0) c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + ch] = v;
+  }
+  zero_pads<NW>(c, o[O_OUT], C);
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_LN: LayerNormalization over channels (two-pass mean/variance in registers, one wave per row,
+// wave64 shuffle reductions).  Training keeps xhat and rstd for OP_LNB.
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_ln(const Ctx& c, const int* o) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int C = slot_w(c, o[O_A], S_C);
+  const int a_off = slot_w(c, o[O_A], S_OFF), a_st = slot_w(c, o[O_A], S_STRIDE);
+  const int o_off = slot_w(c, o[O_OUT], S_OFF), o_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const int goff = o[O_AUX0], boff = o[O_AUX1];
+  const int xs = o[O_AUX2], rs = o[O_AUX3];
+  const float eps = __int_as_float(o[O_F0]);
+  const Epi e = load_epi(o);
+  const float invC = 1.f / (float)C;
+  for (int r = wave; r < c.T; r += NW) {
+    float v[8];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = lane + 64 * j;
+      v[j] = ch < C ? c.lds[a_off + r * a_st + ch] : 0.f;
+      s += v[j];
+    }
+    const float mean = wave_sum(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = lane + 64 * j;
+      const float d = ch < C ? v[j] - mean : 0.f;
+      q += d * d;
+    }
+    const float var = wave_sum(q) * invC;
+    const float rstd = rsqrtf(var + eps);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = lane + 64 * j;
+      if (ch < C) {
+        const float xh = (v[j] - mean) * rstd;
+        float y = xh;
+        if (goff >= 0) y *= c.params[goff + ch];
+        if (boff >= 0) y += c.params[boff + ch];
+        c.lds[o_off + r * o_st + ch] = epi_fwd(c, e, y, r, ch);
+        if (xs >= 0) c.lds[slot_w(c, xs, S_OFF) + r * slot_w(c, xs, S_STRIDE) + ch] = xh;
+      }
+    }
+    if (rs >= 0 && lane == 0) c.lds[slot_w(c, rs, S_OFF) + r * slot_w(c, rs, S_STRIDE)] = rstd;
+  }
+  zero_pads<NW>(c, o[O_OUT], C);
+  if (xs >= 0) zero_pads<NW>(c, xs, C);
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_LOSS: e = pred - y; sum e^2, sum |e| over valid rows; dL/dpred = 2 e / count through the
+// producer's epilogue (mse: train_96.py:51; labels (B,1,1,3) broadcast over H,W)
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_loss(const Ctx& c, const int* o, const float* __restrict__ ytrue,
+                                        const int* __restrict__ idx, float inv_count, bool train,
+                                        float& sse, float& sae) {
+  constexpr int NT = NW * 64;
+  const int N = o[O_N];
+  const int a_off = slot_w(c, o[O_A], S_OFF), a_st = slot_w(c, o[O_A], S_STRIDE);
+  const int g_off = slot_w(c, o[O_OUT], S_OFF), g_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const Epi e = load_epi(o);
+  for (int it = threadIdx.x; it < c.T * N; it += NT) {
+    const int r = it / N, n = it - r * N;
+    const int64_t R = c.row0 + r;
+    const float p = c.lds[a_off + r * a_st + n];
+    float g = 0.f;
+    if (R < c.nrows) {
+      const int64_t img = R / c.P;
+      const int64_t src = idx ? (int64_t)idx[img] : img;
+      const float err = p - ytrue[src * N + n];
+      sse = fmaf(err, err, sse);
+      sae += fabsf(err);
+      g = 2.f * err * inv_count;
+    }
+    if (train) {
+      const float z = e.zslot >= 0 ? c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + n] : 0.f;
+      c.lds[g_off + r * g_st + n] = epi_bwd(c, e, g, p, z, r, n);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_EPIGRAD: out[r][c] <- out[r][c] * epi'(value) in place
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_epigrad(const Ctx& c, const int* o) {
+  constexpr int NT = NW * 64;
+  const int C = slot_w(c, o[O_OUT], S_C);
+  const int v_off = slot_w(c, o[O_A], S_OFF), v_st = slot_w(c, o[O_A], S_STRIDE);
+  const int g_off = slot_w(c, o[O_OUT], S_OFF), g_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const Epi e = load_epi(o);
+  for (int it = threadIdx.x; it < c.T * C; it += NT) {
+    const int r = it / C, ch = it - r * C;
+    const float z = e.zslot >= 0 ? c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + ch] : 0.f;
+    float* gp = c.lds + g_off + r * g_st + ch;
+    *gp = epi_bwd(c, e, *gp, c.lds[v_off + r * v_st + ch], z, r, ch);
+  }
+}
+
+// destination write of a backward result (STORE / ACCUM / EPIGRAD through the producer of `val`)
+__device__ __forceinline__ void dst_write(const Ctx& c, const int* o, int mode, const Epi& e,
+                                          int d_off, int d_st, int v_off, int v_st, int z_off,
+                                          int z_st, int r, int ch, float v) {
+  float* p = c.lds + d_off + r * d_st + ch;
+  if (mode == DST_STORE) *p = v;
+  else if (mode == DST_ACCUM) *p += v;
+  else {
+    const float z = e.zslot >= 0 ? c.lds[z_off + r * z_st + ch] : 0.f;
+    *p = epi_bwd(c, e, v, c.lds[v_off + r * v_st + ch], z, r, ch);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// OP_DIN: out[r][k] (=|+=|epigrad) sum_n a[r][n] W[k][n], reading W^T [N][K] (mirror kept by the
+// optimizer) so B rows stay coalesced.  Same MFMA tiling as OP_DENSE.
+// ------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void op_din(const Ctx& c, const int* o) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int sa = o[O_A], so = o[O_OUT];
+  const int a_off = slot_w(c, sa, S_OFF), a_cp = slot_w(c, sa, S_CP), a_st = slot_w(c, sa, S_STRIDE);
+  const int d_off = slot_w(c, so, S_OFF), d_st = slot_w(c, so, S_STRIDE), d_cp = slot_w(c, so, S_CP);
+  const int K = o[O_K], N = o[O_N], mode = o[O_MODE];
+  const int vs = o[O_AUX0];
+  const int v_off = vs >= 0 ? slot_w(c, vs, S_OFF) : 0, v_st = vs >= 0 ? slot_w(c, vs, S_STRIDE) : 0;
+  const Epi e = load_epi(o);
+  const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0;
+  const int z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+  const float* WT = (o[O_WSEL] ? c.params : c.params_t) + o[O_W];
+  const int nrb = c.T >> 5, ncb = (K + 31) >> 5;
+  const int Nh = a_cp >> 1;
+  const int nbase = half * Nh;
+  const int nval = N - nbase;
+  for (int task = wave; task < nrb * ncb; task += NW) {
+    const int cb = task / nrb, rb = task - cb * nrb;
+    const int k = cb * 32 + l32;
+    const bool kok = k < K;
+    const float* ap = c.lds + a_off + (rb * 32 + l32) * a_st + nbase;
+    const float* bp = WT + (size_t)nbase * K + (kok ? k : 0);
+    f32x16 acc = {};
+    for (int m = 0; m < Nh; m += 4) {
+      const f32x4 a0 = *(const f32x4*)(ap + m);
+      float b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (kok && m + j < nval) ? bp[(size_t)(m + j) * K] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, b[3], acc, 0, 0, 0);
+    }
+    if (kok) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int r = rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        dst_write(c, o, mode, e, d_off, d_st, v_off, v_st, z_off, z_st, r, k, acc[g]);
+      }
+    } else if (mode == DST_STORE && k < d_cp) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c.lds[d_off + (rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * d_st + k] = 0.f;
+    }
+  }
+}
+
+// OP_TDIN: thin contraction (N <= 8): out[r][k] (=|+=|epigrad) sum_n a[r][n] W[k][n]
+template <int NW>
+__device__ __forceinline__ void op_tdin(const Ctx& c, const int* o) {
+  constexpr int NT = NW * 64;
+  const int sa = o[O_A], so = o[O_OUT];
+  const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
+  const int d_off = slot_w(c, so, S_OFF), d_st = slot_w(c, so, S_STRIDE);
+  const int K = o[O_K], N = o[O_N], mode = o[O_MODE];
+  const int vs = o[O_AUX0];
+  const int v_off = vs >= 0 ? slot_w(c, vs, S_OFF) : 0, v_st = vs >= 0 ? slot_w(c, vs, S_STRIDE) : 0;
+  const Epi e = load_epi(o);
+  const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0;
+  const int z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+  const float* W = (o[O_WSEL] ? c.params_t : c.params) + o[O_W];
+  for (int it = threadIdx.x; it < c.T * K; it += NT) {
+    const int r = it / K, k = it - r * K;
+    const float* ap = c.lds + a_off + r * a_st;
+    const float* wp = W + (size_t)k * N;
+    float v = 0.f;
+    for (int n = 0; n < N; ++n) v = fmaf(ap[n], wp[n], v);
+    dst_write(c, o, mode, e, d_off, d_st, v_off, v_st, z_off, z_st, r, k, v);
+  }
+  if (mode == DST_STORE) zero_pads<NW>(c, so, K);
+}
+
+// OP_EWB: backward of OP_EW (its epilogue already applied by OP_EPIGRAD / fused producer)
+template <int NW>
+__device__ __forceinline__ void op_ewb(const Ctx& c, const int* o) {
+  constexpr int NT = NW * 64;
+  const int flags = o[O_FLAGS];
+  const int C = slot_w(c, o[O_OUT], S_C);
+  const int g_off = slot_w(c, o[O_OUT], S_OFF), g_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const int a_off = slot_w(c, o[O_A], S_OFF), a_st = slot_w(c, o[O_A], S_STRIDE);
+  const int hb = flags & EW_HAS_B;
+  const int b_off = hb ? slot_w(c, o[O_B], S_OFF) : 0, b_st = hb ? slot_w(c, o[O_B], S_STRIDE) : 0;
+  const int d0 = o[O_AUX0], d1 = o[O_AUX1];
+  const int d0_off = d0 >= 0 ? slot_w(c, d0, S_OFF) : 0, d0_st = d0 >= 0 ? slot_w(c, d0, S_STRIDE) : 0;
+  const int d1_off = d1 >= 0 ? slot_w(c, d1, S_OFF) : 0, d1_st = d1 >= 0 ? slot_w(c, d1, S_STRIDE) : 0;
+  const int mode = o[O_MODE];  // bit0: d0 accumulate, bit1: d1 accumulate
+  const float f0 = __int_as_float(o[O_F0]), f1 = __int_as_float(o[O_F1]);
+  const int soff = o[O_AUX2];
+  for (int it = threadIdx.x; it < c.T * C; it += NT) {
+    const int r = it / C, ch = it - r * C;
+    float g = c.lds[g_off + r * g_st + ch];
+    if (flags & EW_AFFINE) g *= c.params[soff + ch];
+    float g0, g1 = 0.f;
+    if (flags & EW_MUL) {
+      g0 = g * c.lds[b_off + r * b_st + ch];
+      g1 = g * c.lds[a_off + r * a_st + ch];
+    } else {
+      g0 = f0 * g;
+      g1 = f1 * g;
+    }
+    if (d0 >= 0) {
+      float* p = c.lds + d0_off + r * d0_st + ch;
+      *p = (mode & 1) ? *p + g0 : g0;
+    }
+    if (d1 >= 0) {
+      float* p = c.lds + d1_off + r * d1_st + ch;
+      *p = (mode & 2) ? *p + g1 : g1;
+    }
+  }
+  if (d0 >= 0 && !(mode & 1)) zero_pads<NW>(c, d0, C);
+  if (d1 >= 0 && !(mode & 2)) zero_pads<NW>(c, d1, C);
+}
+
+// OP_LNB: LayerNorm backward, one wave per row
+template <int NW>
+__device__ __forceinline__ void op_lnb(const Ctx& c, const int* o) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int C = slot_w(c, o[O_A], S_C);
+  const int x_off = slot_w(c, o[O_A], S_OFF), x_st = slot_w(c, o[O_A], S_STRIDE);
+  const int g_off = slot_w(c, o[O_B], S_OFF), g_st = slot_w(c, o[O_B], S_STRIDE);
+  const int d_off = slot_w(c, o[O_OUT], S_OFF), d_st = slot_w(c, o[O_OUT], S_STRIDE);
+  const int goff = o[O_AUX0], rs = o[O_AUX1], mode = o[O_MODE];
+  const int rs_off = slot_w(c, rs, S_OFF), rs_st = slot_w(c, rs, S_STRIDE);
+  const float invC = 1.f / (float)C;
+  for (int r = wave; r < c.T; r += NW) {
+    float xh[8], dxh[8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = lane + 64 * j;
+      xh[j] = 0.f;
+      dxh[j] = 0.f;
+      if (ch < C) {
+        xh[j] = c.lds[x_off + r * x_st + ch];
+        dxh[j] = c.lds[g_off + r * g_st + ch] * (goff >= 0 ? c.params[goff + ch] : 1.f);
+      }
+      s1 += dxh[j];
+      s2 += dxh[j] * xh[j];
+    }
+    const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
+    const float rstd = c.lds[rs_off + r * rs_st];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = lane + 64 * j;
+      if (ch < C) {
+        const float v = rstd * (dxh[j] - m1 - xh[j] * m2);
+        float* p = c.lds + d_off + r * d_st + ch;
+        *p = mode == DST_ACCUM ? *p + v : v;
+      }
+    }
+  }
+  if (mode != DST_ACCUM) zero_pads<NW>(c, o[O_OUT], C);
+}
+
+// ------------------------------------------------------------------------------------------------
+// the kernel
+// ------------------------------------------------------------------------------------------------
+struct Args {
+  const int* prog;
+  const float* params;
+  const float* params_t;
+  const float* x;
+  const float* ytrue;
+  const int* idx;
+  float* y;          // forward output
+  float* ws;         // per-workgroup partials (train / eval)
+  int64_t nrows;
+  int P;
+  int64_t img_off;
+  float inv_count;
+  uint64_t seed;
+};
+
+template <int NW, int MAXACC>
+__global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NT = NW * 64;
+  const int* prog = args.prog;
+  const int T = prog[H_T];
+  const int mode = prog[H_MODE];
+  const bool train = mode == MODE_TRAIN;
+  const int nops = prog[H_NOPS];
+  const int ops_off = prog[H_OPS_OFF];
+  const int lds_floats = prog[H_LDS_FLOATS];
+  const int in_slot = prog[H_IN_SLOT], out_slot = prog[H_OUT_SLOT];
+  const int Cin = prog[H_CIN], Cout = prog[H_COUT];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+
+  Ctx c;
+  c.prog = prog;
+  c.params = args.params;
+  c.params_t = args.params_t;
+  c.lds = lds;
+  c.T = T;
+  c.nrows = args.nrows;
+  c.P = args.P;
+  c.img_off = args.img_off;
+  c.seed = args.seed;
+
+  for (int i = threadIdx.x; i < lds_floats; i += NT) lds[i] = 0.f;
+
+  f32x16 dacc[MAXACC];
+#pragma unroll
+  for (int s = 0; s < MAXACC; ++s) dacc[s] = f32x16{};
+  float tacc[MAXTHIN];
+#pragma unroll
+  for (int s = 0; s < MAXTHIN; ++s) tacc[s] = 0.f;
+  float sse = 0.f, sae = 0.f;
+
+  const int in_off = slot_w(c, in_slot, S_OFF), in_st = slot_w(c, in_slot, S_STRIDE);
+  const int64_t ntiles = (args.nrows + T - 1) / T;
+  const int* blk = prog + prog[H_BLK_OFF] + wave * MAXACC;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    c.row0 = tile * T;
+    __syncthreads();
+    // ---- stage the tile's input rows (coalesced 16-B loads, rows contiguous in HBM) ----
+    if ((Cin & 3) == 0) {
+      const int q = Cin >> 2, qp = slot_w(c, in_slot, S_CP) >> 2;  // pad columns written as 0
+      for (int it = threadIdx.x; it < T * qp; it += NT) {
+        const int r = it / qp, j = it - r * qp;
+        const int64_t R = c.row0 + r;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (R < args.nrows && j < q) {
+          const int64_t img = R / args.P, pos = R - img * args.P;
+          const int64_t src = (args.idx ? (int64_t)args.idx[img] : img) * args.P + pos;
+          v = *(const f32x4*)(args.x + src * Cin + 4 * j);
+        }
+        *(f32x4*)(lds + in_off + r * in_st + 4 * j) = v;
+      }
+    } else {
+      const int cp = slot_w(c, in_slot, S_CP);
+      for (int it = threadIdx.x; it < T * cp; it += NT) {
+        const int r = it / cp, j = it - r * cp;
+        const int64_t R = c.row0 + r;
+        float v = 0.f;
+        if (R < args.nrows && j < Cin) {
+          const int64_t img = R / args.P, pos = R - img * args.P;
+          const int64_t src = (args.idx ? (int64_t)args.idx[img] : img) * args.P + pos;
+          v = args.x[src * Cin + j];
+        }
+        lds[in_off + r * in_st + j] = v;
+      }
+    }
+    __syncthreads();
+    for (int oi = 0; oi < nops; ++oi) {
+      const int* o = prog + ops_off + oi * O_WORDS;
+      const int type = o[O_TYPE];
+      switch (type) {
+        case OP_DENSE: op_dense<NW>(c, o); break;
+        case OP_TDENSE: op_tdense<NW>(c, o); break;
+        case OP_EW: op_ew<NW>(c, o); break;
+        case OP_LN: op_ln<NW>(c, o); break;
+        case OP_LOSS:
+          op_loss<NW>(c, o, args.ytrue, args.idx, args.inv_count, train, sse, sae);
+          break;
+        case OP_EPIGRAD: op_epigrad<NW>(c, o); break;
+        case OP_DW: {
+          const int sa = o[O_A], sb = o[O_B];
+          const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
+          const int b_off = slot_w(c, sb, S_OFF), b_st = slot_w(c, sb, S_STRIDE);
+          const int K = o[O_K], N = o[O_N];
+          const int Th = T >> 1;
+#pragma unroll
+          for (int s = 0; s < MAXACC; ++s) {
+            const int ent = blk[s];
+            if (ent >= 0 && (ent >> 16) == oi) {
+              const int kb = (ent >> 8) & 0xff, nb = ent & 0xff;
+              const int k = kb * 32 + l32, n = nb * 32 + l32;
+              const bool kok = k < K, nok = n < N;
+              const float* ap = lds + a_off + (half * Th) * a_st + (kok ? k : 0);
+              const float* bp = lds + b_off + (half * Th) * b_st + (nok ? n : 0);
+              f32x16 acc = dacc[s];
+              for (int m = 0; m < Th; m += 4) {
+                float a[4], b[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  a[j] = kok ? ap[(m + j) * a_st] : 0.f;
+                  b[j] = nok ? bp[(m + j) * b_st] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+              }
+              dacc[s] = acc;
+            }
+          }
+          break;
+        }
+        case OP_TACC: {
+          const int sa = o[O_A], sb = o[O_B];
+          const int a_off = sa >= 0 ? slot_w(c, sa, S_OFF) : 0, a_st = sa >= 0 ? slot_w(c, sa, S_STRIDE) : 0;
+          const int b_off = slot_w(c, sb, S_OFF), b_st = slot_w(c, sb, S_STRIDE);
+          const int N = o[O_N], tm = o[O_AUX3], tb = o[O_TBASE], tn = o[O_TCOUNT];
+#pragma unroll
+          for (int s = 0; s < MAXTHIN; ++s) {
+            const int el = threadIdx.x + s * NT - tb;
+            if (el >= 0 && el < tn) {
+              int ka, nb_;
+              if (tm == TACC_GEMM) { ka = el / N; nb_ = el - ka * N; }
+              else { ka = el; nb_ = el; }
+              const float* ap = lds + a_off + ka;
+              const float* bp = lds + b_off + nb_;
+              float acc = 0.f;
+              if (tm == TACC_BIAS || sa < 0) {
+                for (int r = 0; r < T; ++r) acc += bp[r * b_st];
+              } else {
+                for (int r = 0; r < T; ++r) acc = fmaf(ap[r * a_st], bp[r * b_st], acc);
+              }
+              tacc[s] += acc;
+            }
+          }
+          break;
+        }
+        case OP_DIN: op_din<NW>(c, o); break;
+        case OP_TDIN: op_tdin<NW>(c, o); break;
+        case OP_EWB: op_ewb<NW>(c, o); break;
+        case OP_LNB: op_lnb<NW>(c, o); break;
+        default: break;
+      }
+      __syncthreads();
+    }
+    if (mode == MODE_FWD) {
+      const int o_off = slot_w(c, out_slot, S_OFF), o_st = slot_w(c, out_slot, S_STRIDE);
+      for (int it = threadIdx.x; it < T * Cout; it += NT) {
+        const int r = it / Cout, n = it - r * Cout;
+        const int64_t R = c.row0 + r;
+        if (R < args.nrows) args.y[R * Cout + n] = lds[o_off + r * o_st + n];
+      }
+    }
+  }
+
+  if (mode == MODE_FWD) return;
+  // ---- flush this workgroup's partials: slab[blockIdx] = [dW..., sum e^2, sum |e|] ----
+  const int slab = prog[H_SLAB];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  float* ws = args.ws + (size_t)blockIdx.x * slab;
+  if (train) {
+#pragma unroll
+    for (int s = 0; s < MAXACC; ++s) {
+      const int ent = blk[s];
+      if (ent >= 0) {
+        const int* o = prog + ops_off + (ent >> 16) * O_WORDS;
+        const int K = o[O_K], N = o[O_N], woff = o[O_W];
+        const int kb = (ent >> 8) & 0xff, nb = ent & 0xff;
+        const int n = nb * 32 + l32;
+        if (n < N) {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+            if (k < K) ws[woff + k * N + n] = dacc[s][g];
+          }
+        }
+      }
+    }
+    const int ntacc = prog[H_NTACC];
+    const int* tl = prog + prog[H_TACC_OFF];
+#pragma unroll
+    for (int s = 0; s < MAXTHIN; ++s) {
+      const int e = threadIdx.x + s * NT;
+      for (int q = 0; q < ntacc; ++q) {
+        const int* o = prog + ops_off + tl[q] * O_WORDS;
+        const int el = e - o[O_TBASE];
+        if (el >= 0 && el < o[O_TCOUNT]) ws[o[O_W] + el] = tacc[s];
+      }
+    }
+  }
+  // block reduction of the loss sums (fixed order)
+  float* red = lds + lds_floats;  // 2 x NW floats past the program's LDS (all LDS in one array)
+  const float a = wave_sum(sse), b = wave_sum(sae);
+  __syncthreads();
+  if (lane == 0) { red[wave] = a; red[NW + wave] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int w = 0; w < NW; ++w) { s0 += red[w]; s1 += red[NW + w]; }
+    ws[npt] = s0;
+    ws[npt + 1] = s1;
+  }
+}
+
+// grad[i] = sum_g ws[g][i]  (fixed order over workgroups)
+__global__ void reduce_kernel(const float* __restrict__ ws, float* __restrict__ grad, int grid,
+                              int slab, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int g = 0; g < grid; ++g) s += ws[(size_t)g * slab + i];
+  grad[i] = s;
+}
+
+// Keras legacy optimizers (TF ApplyGradientDescent / ApplyAdam / ApplyAdaMax functors)
+__global__ void optim_kernel(int kind, float lr, float alpha, float b1, float b2, float eps,
+                             float gscale, float* __restrict__ w, float* __restrict__ wt,
+                             float* __restrict__ m, float* __restrict__ v,
+                             const float* __restrict__ grad, const float* __restrict__ l2,
+                             const int* __restrict__ tpos, int64_t n, float* __restrict__ regp) {
+  float reg = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float wi = w[i];
+    const float c2 = l2[i];
+    reg = fmaf(c2 * wi, wi, reg);
+    const float g = fmaf(grad[i], gscale, 2.f * c2 * wi);
+    float wn;
+    if (kind == HPE_OPT_SGD) {
+      wn = wi - lr * g;
+    } else if (kind == HPE_OPT_ADAM) {
+      float mi = m[i], vi = v[i];
+      mi += (g - mi) * (1.f - b1);
+      vi += (g * g - vi) * (1.f - b2);
+      m[i] = mi;
+      v[i] = vi;
+      wn = wi - (mi * alpha) / (sqrtf(vi) + eps);
+    } else {
+      float mi = m[i], vi = v[i];
+      mi += (g - mi) * (1.f - b1);
+      vi = fmaxf(b2 * vi, fabsf(g));
+      m[i] = mi;
+      v[i] = vi;
+      wn = wi - alpha * (mi / (vi + eps));
+    }
+    w[i] = wn;
+    const int tp = tpos[i];
+    if (tp >= 0) wt[tp] = wn;
+  }
+  reg = wave_sum(reg);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = reg;
+  __syncthreads();
+  if (threadIdx.x == 0) regp[2 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the step's loss sums (post all-reduce)
+    regp[0] = grad[n];
+    regp[1] = grad[n + 1];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+static thread_local char g_err[512];
+
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIPCHK(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) return fail(HPE_ERUNTIME, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+struct hpe_program {
+  int* dwords;
+  int hdr[H_WORDS];
+  int n_cu;
+  int grid_cap;
+};
+
+extern "C" const char* hpe_last_error(void) { return g_err; }
+
+typedef void (*kfn_t)(Args);
+
+template <int NW>
+static kfn_t pick_acc(int maxacc) {
+  if (maxacc <= 1) return rowprog_kernel<NW, 1>;
+  if (maxacc <= 2) return rowprog_kernel<NW, 2>;
+  if (maxacc <= 4) return rowprog_kernel<NW, 4>;
+  if (maxacc <= 8) return rowprog_kernel<NW, 8>;
+  return nullptr;
+}
+
+static kfn_t pick_kernel(int nw, int maxacc) {
+  switch (nw) {
+    case 4: return pick_acc<4>(maxacc);
+    case 8: return pick_acc<8>(maxacc);
+    case 12: return pick_acc<12>(maxacc);
+    case 16: return pick_acc<16>(maxacc);
+    default: return nullptr;
+  }
+}
+
+extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_program** out) {
+  if (!words || !out || n_words < H_WORDS) return fail(HPE_EINVAL, "program: null or short word stream");
+  if (words[H_MAGIC] != HPE_MAGIC) return fail(HPE_EINVAL, "program: bad magic");
+  const int nw = words[H_NW], T = words[H_T];
+  if (T <= 0 || T % 32) return fail(HPE_EINVAL, "program: T=%d must be a positive multiple of 32", T);
+  if (!pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
+  if (words[H_MAXTHIN] > MAXTHIN) return fail(HPE_EINVAL, "program: MAXTHIN=%d > %d", words[H_MAXTHIN], MAXTHIN);
+  if ((int64_t)(words[H_LDS_FLOATS] + 32) * 4 > 160 * 1024) return fail(HPE_EINVAL, "program: LDS %d floats exceeds 160 KiB", words[H_LDS_FLOATS]);
+  hpe_program* p = new hpe_program();
+  memcpy(p->hdr, words, sizeof(p->hdr));
+  hipError_t e = hipMalloc(&p->dwords, n_words * sizeof(int32_t));
+  if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
+  e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { hipFree(p->dwords); delete p; return fail(HPE_ERUNTIME, "hipMemcpy: %s", hipGetErrorString(e)); }
+  int dev = 0;
+  hipGetDevice(&dev);
+  int ncu = 256;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  p->n_cu = ncu;
+  const int lds_bytes = (words[H_LDS_FLOATS] + 32) * 4;
+  int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
+  const int by_waves = 32 / nw;
+  if (per_cu > by_waves) per_cu = by_waves;
+  if (words[H_WG_PER_CU] > 0 && per_cu > words[H_WG_PER_CU]) per_cu = words[H_WG_PER_CU];
+  if (per_cu < 1) per_cu = 1;
+  p->grid_cap = ncu * per_cu;
+  kfn_t k = pick_kernel(nw, words[H_MAXACC]);
+  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (words[H_LDS_FLOATS] + 32) * 4);
+  *out = p;
+  return HPE_OK;
+}
+
+extern "C" int hpe_program_destroy(hpe_program* p) {
+  if (!p) return HPE_OK;
+  hipFree(p->dwords);
+  delete p;
+  return HPE_OK;
+}
+
+extern "C" int hpe_launch_grid(const hpe_program* p, int64_t n_rows) {
+  if (!p) return 0;
+  const int64_t ntiles = (n_rows + p->hdr[H_T] - 1) / p->hdr[H_T];
+  int64_t g = ntiles < p->grid_cap ? ntiles : p->grid_cap;
+  return (int)(g < 1 ? 1 : g);
+}
+
+extern "C" size_t hpe_workspace_size(const hpe_program* p, int64_t n_rows) {
+  if (!p) return 0;
+  return (size_t)hpe_launch_grid(p, n_rows) * p->hdr[H_SLAB] * sizeof(float);
+}
+
+static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
+  kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC]);
+  const int grid = hpe_launch_grid(p, nrows);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), (p->hdr[H_LDS_FLOATS] + 32) * 4, s, a);
+  HIPCHK(hipGetLastError());
+  return HPE_OK;
+}
+
+extern "C" int hpe_forward(const hpe_program* p, const float* params, const float* params_t,
+                           const float* x, int64_t n_images, int32_t P, const int32_t* idx,
+                           float* y, void* stream) {
+  if (!p || !params || !x || !y) return fail(HPE_EINVAL, "hpe_forward: null argument");
+  if (p->hdr[H_MODE] != MODE_FWD) return fail(HPE_EINVAL, "hpe_forward: program not compiled for inference");
+  if (n_images < 0 || P <= 0) return fail(HPE_EINVAL, "hpe_forward: bad shape n_images=%lld P=%d", (long long)n_images, P);
+  if (n_images == 0) return HPE_OK;
+  Args a = {};
+  a.prog = p->dwords; a.params = params; a.params_t = params_t ? params_t : params; a.x = x;
+  a.idx = idx; a.y = y; a.nrows = n_images * (int64_t)P; a.P = P;
+  return launch(p, a, a.nrows, (hipStream_t)stream);
+}
+
+extern "C" int hpe_train_step(const hpe_program* p, const float* params, const float* params_t,
+                              const float* x, const float* ytrue, int64_t n_images, int32_t P,
+                              const int32_t* idx, int64_t img_off, float inv_count, uint64_t seed,
+                              void* ws, void* stream) {
+  if (!p || !params || !x || !ytrue || !ws) return fail(HPE_EINVAL, "hpe_train_step: null argument");
+  if (p->hdr[H_MODE] == MODE_FWD) return fail(HPE_EINVAL, "hpe_train_step: program compiled for inference only");
+  if (n_images <= 0 || P <= 0) return fail(HPE_EINVAL, "hpe_train_step: bad shape n_images=%lld P=%d", (long long)n_images, P);
+  Args a = {};
+  a.prog = p->dwords; a.params = params; a.params_t = params_t ? params_t : params; a.x = x;
+  a.ytrue = ytrue; a.idx = idx; a.ws = (float*)ws; a.nrows = n_images * (int64_t)P; a.P = P;
+  a.img_off = img_off; a.inv_count = inv_count; a.seed = seed;
+  return launch(p, a, a.nrows, (hipStream_t)stream);
+}
+
+extern "C" int hpe_reduce(const hpe_program* p, int64_t n_rows, const void* ws, float* grad, void* stream) {
+  if (!p || !ws || !grad) return fail(HPE_EINVAL, "hpe_reduce: null argument");
+  const int grid = hpe_launch_grid(p, n_rows);
+  const int n = p->hdr[H_NPARAMS_TRAIN] + 4;
+  hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)ws, grad, grid, p->hdr[H_SLAB], n);
+  HIPCHK(hipGetLastError());
+  return HPE_OK;
+}
+
+extern "C" int hpe_optim_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  return (int)(g < 1 ? 1 : g);
+}
+
+extern "C" int hpe_optim_step(int32_t kind, float lr, float b1, float b2, float eps, int64_t iter,
+                              float gscale, float* w, float* wt, float* m, float* v,
+                              const float* grad, const float* l2, const int32_t* tpos, int64_t n,
+                              float* regp, void* stream) {
+  if (!w || !grad || !l2 || !tpos || !regp) return fail(HPE_EINVAL, "hpe_optim_step: null argument");
+  if (kind != HPE_OPT_SGD && (!m || !v)) return fail(HPE_EINVAL, "hpe_optim_step: Adam/Adamax need m and v");
+  if (iter < 1) return fail(HPE_EINVAL, "hpe_optim_step: iter must be >= 1");
+  double alpha = lr;
+  if (kind == HPE_OPT_ADAM) {
+    const double b1p = pow((double)b1, (double)iter), b2p = pow((double)b2, (double)iter);
+    alpha = (double)lr * sqrt(1.0 - b2p) / (1.0 - b1p);
+  } else if (kind == HPE_OPT_ADAMAX) {
+    alpha = (double)lr / (1.0 - pow((double)b1, (double)iter));
+  } else if (kind != HPE_OPT_SGD) {
+    return fail(HPE_EINVAL, "hpe_optim_step: unknown optimizer kind %d", kind);
+  }
+  const int grid = hpe_optim_grid(n);
+  hipLaunchKernelGGL(optim_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, kind, lr,
+                     (float)alpha, b1, b2, eps, gscale, w, wt ? wt : w, m, v, grad, l2, tpos, n, regp);
+  HIPCHK(hipGetLastError());
+  return HPE_OK;
+}

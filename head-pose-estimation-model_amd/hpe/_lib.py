@@ -1,0 +1,58 @@
+"""ctypes binding of libhpe.so (include/hpe.h).  The library is built in-tree by
+``__graft_entry__.build()`` (hipcc --offload-arch=gfx950); there is no fallback: every compute
+call goes through these symbols, and a missing library raises at first use."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libhpe.so')
+
+# symbol -> (restype, argtypes), exactly the declarations of include/hpe.h
+_vp, _i32, _i64, _f, _u64, _sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
+                                  ctypes.c_uint64, ctypes.c_size_t)
+SIGNATURES = {
+    'hpe_program_create': (ctypes.c_int, [_vp, _i64, ctypes.POINTER(_vp)]),
+    'hpe_program_destroy': (ctypes.c_int, [_vp]),
+    'hpe_launch_grid': (ctypes.c_int, [_vp, _i64]),
+    'hpe_workspace_size': (_sz, [_vp, _i64]),
+    'hpe_forward': (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
+    'hpe_train_step': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _f, _u64,
+                                      _vp, _vp]),
+    'hpe_reduce': (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp]),
+    'hpe_optim_step': (ctypes.c_int, [_i32, _f, _f, _f, _f, _i64, _f, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _i64, _vp, _vp]),
+    'hpe_optim_grid': (ctypes.c_int, [_i64]),
+    'hpe_last_error': (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class HPEError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libhpe.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HPEError('libhpe.so not found at %s: run __graft_entry__.build() (hipcc gfx950)'
+                       % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=''):
+    if rc == 0:
+        return
+    msg = load().hpe_last_error().decode(errors='replace')
+    if rc == 1:
+        raise ValueError('%s: %s' % (what, msg))
+    raise HPEError('%s: %s' % (what, msg))

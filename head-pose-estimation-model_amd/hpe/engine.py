@@ -1,0 +1,166 @@
+"""Device-side execution of one model: compiled row programs, parameter / optimizer buffers, and
+the per-step launch sequence (train_step -> reduce -> [RCCL all-reduce] -> optimizer).
+
+PyTorch is used only for device memory, the current HIP stream and torch.distributed (RCCL); every
+arithmetic op of the hot path runs in libhpe.so (csrc/hpe_rowprog.hip) through the C ABI.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .compiler import build_mirror, compile_graph
+
+OPT_KIND = {'sgd': 0, 'adam': 1, 'adamax': 2}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class _Compiled:
+    def __init__(self, prog):
+        self.prog = prog
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        w = np.ascontiguousarray(prog.words, dtype=np.int32)
+        _lib.check(lib.hpe_program_create(w.ctypes.data_as(ctypes.c_void_p), w.size, ctypes.byref(h)),
+                   'hpe_program_create')
+        self.h = h
+        self.ws = None
+        self.ws_rows = -1
+
+    def workspace(self, n_rows, device):
+        lib = _lib.load()
+        need = lib.hpe_workspace_size(self.h, n_rows)
+        if self.ws is None or self.ws.numel() * 4 < need:
+            # zero once: slab entries no op owns stay zero for ever
+            self.ws = torch.zeros(max(need // 4, 4), dtype=torch.float32, device=device)
+        return self.ws
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.load().hpe_program_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Engine:
+    """Parameters live on the device as one flat fp32 vector in Keras trainable_weights order
+    (+ inference constants), plus the transposed mirror the backward GEMMs read."""
+
+    def __init__(self, model_config, weights, device=None):
+        if not torch.cuda.is_available():
+            raise _lib.HPEError('hpe needs a ROCm GPU (MI355X / gfx950); torch.cuda is unavailable')
+        self.device = torch.device(device or 'cuda')
+        self.model_config = model_config
+        self.weights = dict(weights)
+        self.progs = {}
+        base = compile_graph(model_config, self.weights, mode='fwd')
+        self.layout = base
+        flat = np.zeros(base.n_train, dtype=np.float32)
+        for k, (o, shp) in base.param_index.items():
+            flat[o:o + int(np.prod(shp))] = np.asarray(self.weights[k], dtype=np.float32).ravel()
+        self.n_train = base.n_train
+        self.params = torch.from_numpy(np.concatenate([flat, base.consts])).to(self.device)
+        self.params_t = torch.from_numpy(build_mirror(base, flat)).to(self.device)
+        self.l2 = torch.from_numpy(base.l2).to(self.device)
+        self.tpos = torch.from_numpy(base.tpos).to(self.device)
+        self.m = None
+        self.v = None
+        self.iterations = 0
+        self.grad = torch.zeros(self.n_train + 4, dtype=torch.float32, device=self.device)
+
+    # -- programs -----------------------------------------------------------------------------
+    def program(self, mode, P=1):
+        key = (mode, P == 1)
+        if key not in self.progs:
+            prog = compile_graph(self.model_config, self.weights, mode=mode, P=P)
+            if prog.n_train != self.n_train:
+                raise RuntimeError('parameter layout mismatch between programs')
+            if prog.consts.size and self.params.numel() != self.n_train + prog.consts.size:
+                self.params = torch.cat([self.params[:self.n_train],
+                                         torch.from_numpy(prog.consts).to(self.device)])
+            self.progs[key] = _Compiled(prog)
+        return self.progs[key]
+
+    # -- host <-> device weights --------------------------------------------------------------
+    def get_weights(self):
+        flat = self.params[:self.n_train].detach().cpu().numpy()
+        out = {}
+        for k, (o, shp) in self.layout.param_index.items():
+            out[k] = flat[o:o + int(np.prod(shp))].reshape(shp).copy()
+        return out
+
+    def set_weights(self, wdict):
+        flat = self.params[:self.n_train].detach().cpu().numpy().copy()
+        for k, a in wdict.items():
+            o, shp = self.layout.param_index[k]
+            a = np.asarray(a, dtype=np.float32)
+            if a.shape != tuple(shp):
+                raise ValueError('weight %s: shape %s != %s' % (k, a.shape, tuple(shp)))
+            flat[o:o + a.size] = a.ravel()
+        self.params[:self.n_train].copy_(torch.from_numpy(flat))
+        self.params_t.copy_(torch.from_numpy(build_mirror(self.layout, flat)))
+        self.weights.update({k: np.asarray(v, dtype=np.float32) for k, v in wdict.items()})
+
+    # -- compute ------------------------------------------------------------------------------
+    def forward(self, x, P, idx=None, out=None):
+        """x: device fp32 [n_images*P, C_in] (rows); returns [n_images*P, C_out]."""
+        c = self.program('fwd', P)
+        n_img = x.shape[0] // P if idx is None else idx.numel()
+        if out is None:
+            out = torch.empty((n_img * P, c.prog.C_out), dtype=torch.float32, device=self.device)
+        lib = _lib.load()
+        _lib.check(lib.hpe_forward(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), n_img, P,
+                                   _ptr(idx), _ptr(out), _stream()), 'hpe_forward')
+        return out
+
+    def loss_sums(self, x, y, P, idx=None, n_images=None):
+        """Eval pass: returns device tensor [sum e^2, sum |e|, ...] (grad buffer layout)."""
+        c = self.program('eval', P)
+        n_img = n_images if n_images is not None else (x.shape[0] // P if idx is None else idx.numel())
+        lib = _lib.load()
+        ws = c.workspace(n_img * P, self.device)
+        _lib.check(lib.hpe_train_step(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), _ptr(y),
+                                      n_img, P, _ptr(idx), 0, 1.0, 0, _ptr(ws), _stream()),
+                   'hpe_train_step(eval)')
+        out = torch.empty(self.n_train + 4, dtype=torch.float32, device=self.device)
+        _lib.check(lib.hpe_reduce(c.h, n_img * P, _ptr(ws), _ptr(out), _stream()), 'hpe_reduce')
+        return out[self.n_train:self.n_train + 2]
+
+    def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0):
+        """fwd + loss + bwd over this rank's images; self.grad = [dL/dparams..., sse, sae, 0, 0]."""
+        c = self.program('train', P)
+        lib = _lib.load()
+        ws = c.workspace(n_images * P, self.device)
+        _lib.check(lib.hpe_train_step(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), _ptr(y),
+                                      n_images, P, _ptr(idx), img_off, float(inv_count),
+                                      int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(ws), _stream()),
+                   'hpe_train_step')
+        _lib.check(lib.hpe_reduce(c.h, n_images * P, _ptr(ws), _ptr(self.grad), _stream()),
+                   'hpe_reduce')
+        return self.grad
+
+    def optimizer_step(self, opt, stats, grad_scale=1.0):
+        kind = OPT_KIND[opt.kind]
+        if kind and self.m is None:
+            self.m = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+            self.v = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+        self.iterations += 1
+        lib = _lib.load()
+        _lib.check(lib.hpe_optim_step(kind, float(opt.learning_rate), float(opt.beta_1),
+                                      float(opt.beta_2), float(opt.epsilon), self.iterations,
+                                      float(grad_scale), _ptr(self.params), _ptr(self.params_t),
+                                      _ptr(self.m), _ptr(self.v), _ptr(self.grad), _ptr(self.l2),
+                                      _ptr(self.tpos), self.n_train, _ptr(stats), _stream()),
+                   'hpe_optim_step')
+
+    def optim_grid(self):
+        return _lib.load().hpe_optim_grid(self.n_train)

@@ -1,0 +1,102 @@
+/* hpe.h — C ABI of libhpe.so, the MI355X (gfx950) head-pose regression hot path.
+ *
+ * The reference (Maaz77/Head-Pose-Estimation-Model) has no native code and no FFI: its boundary is
+ * the Python/Keras API at the call sites below.  This ABI is what that Keras layer
+ * bottoms out in once TF's CPU kernels are replaced; the Python host package
+ * (head-pose-estimation-model_amd/hpe) binds it with ctypes and keeps the reference's surface.
+ *
+ *   hpe_program_create / _destroy   replaces keras.Model construction + compile
+ *                                   (Model-96/train_96.py:65-110, Model-88/train_88.py:66-253,
+ *                                    Model-88/attention_model.py:16-169): a compiled "row program"
+ *                                    (per-position op list over a tile of rows kept in LDS)
+ *   hpe_forward                     replaces model.predict (Model-96/test.py:34) and the forward of
+ *                                   model.evaluate (train_96.py:186-187)
+ *   hpe_train_step                  replaces one step of model.fit (train_96.py:175-183,
+ *                                   train_88.py:355-363): forward + MSE + backward, per-workgroup
+ *                                   gradient partials into the workspace
+ *   hpe_reduce                      sums the per-workgroup partials into one flat gradient
+ *                                   (the buffer RCCL all-reduces across ranks)
+ *   hpe_optim_step                  replaces optimizer.apply_gradients of Keras' legacy SGD / Adam /
+ *                                   Adamax (train_96.py:99-103, train_88.py:323) + the L2 penalty
+ *                                   gradient of kernel_/bias_regularizer (train_96.py:78-79,90-91)
+ *
+ * Conventions: every buffer is a caller-owned DEVICE pointer (fp32 unless noted); every call is
+ * stream-ordered on the hipStream_t passed as `stream` (0 = null stream) and never synchronises,
+ * allocates or frees (graph-capturable).  Return value 0 = OK; otherwise hpe_last_error() (thread
+ * local) holds the message.  Handles are not thread-safe; one per device.
+ */
+#ifndef HPE_H
+#define HPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hpe_program hpe_program;
+
+/* Error codes */
+#define HPE_OK 0
+#define HPE_EINVAL 1   /* bad argument / shape (the Python layer raises ValueError) */
+#define HPE_ERUNTIME 2 /* HIP runtime failure (RuntimeError) */
+
+/* Optimizer kinds (Keras legacy optimizers) */
+#define HPE_OPT_SGD 0
+#define HPE_OPT_ADAM 1
+#define HPE_OPT_ADAMAX 2
+
+/* Create a program from the int32 word stream produced by hpe/compiler.py (layout documented in
+ * csrc/hpe_prog.h).  Copies the words to device memory owned by the handle. */
+int hpe_program_create(const int32_t *words, int64_t n_words, hpe_program **out);
+int hpe_program_destroy(hpe_program *prog);
+
+/* Number of workgroups a launch over n_rows rows uses, and the workspace bytes hpe_train_step
+ * needs for it: grid x (n_params + 4) floats of per-workgroup partials. */
+int hpe_launch_grid(const hpe_program *prog, int64_t n_rows);
+size_t hpe_workspace_size(const hpe_program *prog, int64_t n_rows);
+
+/* Forward over n_images images of P positions each (rows = n_images * P, channels-last rows of
+ * C_in floats).  image_index (int32, may be NULL) gathers images: row r reads image
+ * image_index[r / P].  y: n_images * P * C_out floats, channel order yaw, pitch, roll. */
+int hpe_forward(const hpe_program *prog, const float *params, const float *params_t,
+                const float *x, int64_t n_images, int32_t P, const int32_t *image_index,
+                float *y, void *stream);
+
+/* One training (or, with a program compiled for evaluation, loss-only) pass.  y_true: per-image
+ * labels [n_images_total][C_out] indexed like x.  image_offset: global index of this rank's first
+ * image (dropout hash).  inv_count: 1 / (global rows * C_out), the MSE normaliser.  workspace:
+ * hpe_workspace_size() bytes; receives per-workgroup partial gradients and [sum e^2, sum |e|]. */
+int hpe_train_step(const hpe_program *prog, const float *params, const float *params_t,
+                   const float *x, const float *y_true, int64_t n_images, int32_t P,
+                   const int32_t *image_index, int64_t image_offset, float inv_count,
+                   uint64_t dropout_seed, void *workspace, void *stream);
+
+/* grad[i] = sum over workgroups of workspace partials, i < n_params + 4 (fixed order). */
+int hpe_reduce(const hpe_program *prog, int64_t n_rows, const void *workspace, float *grad,
+               void *stream);
+
+/* Keras legacy optimizer step on the flat parameter vector:
+ *   g = grad[i] * grad_scale + 2 * l2[i] * w[i]
+ *   SGD:    w -= lr g
+ *   Adam:   m += (g - m)(1-b1); v += (g^2 - v)(1-b2); w -= alpha m / (sqrt(v) + eps),
+ *           alpha = lr sqrt(1-b2^t) / (1-b1^t)
+ *   Adamax: m += (g - m)(1-b1); v = max(b2 v, |g|); w -= lr/(1-b1^t) m / (v + eps)
+ * t = iter (1-based).  tpos[i] >= 0 mirrors the new w[i] into params_t[tpos[i]] (the transposed
+ * copy the backward GEMMs read).  grad holds n + 4 floats (the step's [sum e^2, sum |e|] follow
+ * the gradient).  stats receives [grad[n], grad[n+1], reg_0 .. reg_{grid-1}] where reg_b is block
+ * b's share of sum l2[i] w[i]^2 on the pre-update weights (the Keras regularisation loss). */
+int hpe_optim_step(int32_t kind, float lr, float beta_1, float beta_2, float epsilon, int64_t iter,
+                   float grad_scale, float *params, float *params_t, float *m, float *v,
+                   const float *grad, const float *l2, const int32_t *tpos, int64_t n,
+                   float *stats, void *stream);
+/* Blocks hpe_optim_step launches (stats holds 2 + this many floats). */
+int hpe_optim_grid(int64_t n);
+
+const char *hpe_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HPE_H */

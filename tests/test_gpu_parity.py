@@ -1,0 +1,138 @@
+"""GPU parity: the HIP path (libhpe.so through the C ABI) against the oracle on the reference's
+own TF-trained checkpoints and datasets.  Forward tolerance rtol 1e-5 / atol 1e-4
+degrees; MAE within 1e-4 degrees of the golden; training trajectories within the stated bounds."""
+import numpy as np
+import pytest
+import torch
+
+import hpe
+from hpe import keras
+from oracle import keras_ref as K
+from util import ATOL, RTOL, DATA, features, fixture, index, input_channels, labels
+
+pytestmark = pytest.mark.gpu
+
+FWD_IDS = sorted(r for r in index() if not r.startswith('reg1'))
+
+
+@pytest.mark.parametrize('rid', FWD_IDS)
+def test_forward_every_checkpoint_signature(rid):
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    x = features(301, c, seed=len(rid))
+    ref = K.Graph(mc, w).forward(x).detach().numpy().reshape(-1, 3)
+    got = hpe.model_from_config(mc, w).predict(x).reshape(-1, 3)
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+
+
+GOLDEN_MAE = [  # BASELINE.md §2 (survey restatement of the reference's checkpoints on its data)
+    ('stoqa9pt', 'AFLW2000_features_88_0.7_1.npz', 44.8263),
+    ('stoqa9pt', 'AFLW2000_Enlarged_features_88_0.7_1.npz', 7.8100),
+    ('stoqa9pt', 'BIWI_Test_Enlarged_features_88_0.7_1.npz', 3.4456),
+    ('ker7z9mv', 'AFLW2000_Enlarged_features_88_0.7_1.npz', 7.9921),
+    ('9w31h50k', 'AFLW2000_Enlarged_features_88_0.7_1.npz', 8.3447),
+    ('hrchr82r', 'AFLW2000_features_96_0.7_1.npz', 8.0307),
+    ('model_runid_hrchr82r', 'AFLW2000_features_96_0.7_1.npz', 8.0307),
+    ('sqnu665j', 'AFLW2000_features_96_0.7_1.npz', 7.7826),
+    ('o6e5xpan', 'AFLW2000_features_96_0.7_1.npz', 7.7222),
+]
+
+
+@pytest.mark.parametrize('rid,ds,golden', GOLDEN_MAE)
+def test_golden_mae(rid, ds, golden):
+    mc, w = fixture(rid)
+    d = np.load(DATA + '/' + ds)
+    x, y = d['features'], d['poses']
+    m = hpe.model_from_config(mc, w)
+    p = m.predict(x.reshape(-1, 1, 1, x.shape[1])).reshape(-1, 3)
+    mae = np.mean(np.abs(p - y), axis=0)
+    assert abs(float(np.mean(mae)) - golden) <= 1e-4 + 5e-5, (mae, golden)
+    ref = K.Graph(mc, w).forward(x.reshape(-1, 1, 1, x.shape[1])).detach().numpy().reshape(-1, 3)
+    np.testing.assert_allclose(p, ref, rtol=RTOL, atol=ATOL)
+
+
+TRAIN_CASES = [
+    ('sqnu665j', 'adam', 64, 3),      # create_model(360): 96-360 tanh-3
+    ('0g73t16n', 'adam', 100, 2),     # create_model(256)
+    ('hrchr82r', 'sgd', 128, 3),      # 96-32-16-3
+    ('stoqa9pt', 'adam', 512, 2),     # 88-64 softsign-3, dropout 1e-4
+    ('9w31h50k', 'adamax', 77, 2),    # create_model_complex: residual blocks
+    ('ker7z9mv', 'adam', 50, 2),      # SE + MHA + LayerNorm head (P=1)
+    ('o6e5xpan', 'sgd', 64, 2),       # SeparableConv2D
+]
+
+
+def _oracle_fit(mc, w, opt, x, y, bs, epochs):
+    g = K.Graph(mc, w)
+    o = K.LegacyOptimizer(opt, 2.8e-4 if opt != 'sgd' else 0.05)
+    n = x.shape[0]
+    it = 0
+    for _ in range(epochs):               # shuffle=False: batches in order, last one partial
+        for b0 in range(0, n, bs):
+            it += 1
+            K.train_step(g, o, x[b0:b0 + bs], y[b0:b0 + bs], drop_seed=hpe.random.dropout_seed(it))
+    return g
+
+
+@pytest.mark.parametrize('rid,opt,bs,epochs', TRAIN_CASES)
+def test_training_trajectory(rid, opt, bs, epochs):
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    n = 200
+    x = features(n, c, seed=3)
+    y = labels(n, seed=4)
+    hpe.set_seed(7)
+    m = hpe.model_from_config(mc, w)
+    lr = 2.8e-4 if opt != 'sgd' else 0.05
+    m.compile(optimizer={'adam': keras.optimizers.Adam, 'sgd': keras.optimizers.SGD,
+                         'adamax': keras.optimizers.Adamax}[opt](learning_rate=lr),
+              loss='mse', metrics=['mae'])
+    hist = m.fit(x, y, batch_size=bs, epochs=epochs, shuffle=False, verbose=0)
+    g = _oracle_fit(mc, w, opt, x, y, bs, epochs)
+    got = m.weights_dict()
+    for k in g.trainable:
+        ref = g.params[k].detach().numpy()
+        np.testing.assert_allclose(got[k], ref, rtol=2e-4, atol=2e-5, err_msg=k)
+    pr = m.predict(x).reshape(-1, 3)
+    pref = g.forward(x).detach().numpy().reshape(-1, 3)
+    np.testing.assert_allclose(pr, pref, rtol=1e-4, atol=1e-3)
+    assert np.isfinite(hist.history['loss']).all()
+
+
+def test_spatial_forward_96x96():
+    """Fully-convolutional head on a literal 96x96 map (P = 9216 rows per image)."""
+    mc, w = fixture('hrchr82r')
+    x = features(2, 96, seed=5, h=96, w=96)
+    ref = K.Graph(mc, w).forward(x).detach().numpy()
+    got = hpe.model_from_config(mc, w).predict(x)
+    assert got.shape == (2, 96, 96, 3)
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+
+
+def test_spatial_train_step_grad():
+    """One training step at P = 16x16 against autodiff (labels broadcast over H, W)."""
+    mc, w = fixture('sqnu665j')
+    x = features(6, 96, seed=6, h=16, w=16)
+    y = labels(6, seed=7)
+    m = hpe.model_from_config(mc, w)
+    m.compile(optimizer=keras.optimizers.SGD(learning_rate=0.5), loss='mse', metrics=['mae'])
+    m.fit(x, y, batch_size=6, epochs=1, shuffle=False, verbose=0)
+    g = K.Graph(mc, w)
+    K.train_step(g, K.LegacyOptimizer('sgd', 0.5), x, y, drop_seed=hpe.random.dropout_seed(1))
+    got = m.weights_dict()
+    for k in g.trainable:
+        np.testing.assert_allclose(got[k], g.params[k].numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_evaluate_matches_oracle():
+    mc, w = fixture('stoqa9pt')
+    d = np.load(DATA + '/AFLW2000_Enlarged_features_88_0.7_1.npz')
+    x, y = d['features'].reshape(-1, 1, 1, 88), d['poses']
+    m = hpe.model_from_config(mc, w)
+    m.compile(optimizer=keras.optimizers.SGD(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    loss, mae = m.evaluate(x, y.reshape(-1, 1, 1, 3))
+    g = K.Graph(mc, w)
+    p = g.forward(x).detach().numpy().reshape(-1, 3)
+    ref_mse = float(np.mean((p - y) ** 2)) + float(g.regularization().item())
+    assert abs(loss - ref_mse) <= 1e-4 * ref_mse
+    assert abs(mae - float(np.mean(np.abs(p - y)))) <= 1e-4
