@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 kernel trace + separate PMC passes (FETCH_SIZE, WRITE_SIZE) of bench.py (run via gpurun)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ARGS=${ARGS:---steps 10 --warmup 2 --no-cpu}
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o trace --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/prof_fetch -o fetch --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_fetch.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/prof_write -o write --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_write.log 2>&1
+rc=$?
+echo "rc=$rc"
+exit $rc
