@@ -1,0 +1,141 @@
+// hpe_common.h — device helpers shared by the row-program interpreter and the fused kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hpe_prog.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MAXTHIN 4
+
+// ------------------------------------------------------------------------------------------------
+// activations and their derivatives (derivative from the stored output where possible)
+// ------------------------------------------------------------------------------------------------
+#define SELU_ALPHA 1.6732632423543772848170429916717f
+#define SELU_SCALE 1.0507009873554804934193349852946f
+
+__device__ __forceinline__ float act_f(int act, float z) {
+  switch (act) {
+    case ACT_TANH: return tanhf(z);
+    case ACT_RELU: return z > 0.f ? z : 0.f;
+    case ACT_SOFTSIGN: return z / (1.f + fabsf(z));
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-z));
+    case ACT_ELU: return z > 0.f ? z : expm1f(z);
+    case ACT_SELU: return SELU_SCALE * (z > 0.f ? z : SELU_ALPHA * expm1f(z));
+    case ACT_SWISH: return z / (1.f + expf(-z));
+    case ACT_SOFTPLUS: return z > 20.f ? z : log1pf(expf(z));
+    case ACT_LEAKY_RELU: return z > 0.f ? z : 0.2f * z;
+    default: return z;
+  }
+}
+
+// d act / dz given a = act(z) (and z for swish)
+__device__ __forceinline__ float act_grad(int act, float a, float z) {
+  switch (act) {
+    case ACT_TANH: return 1.f - a * a;
+    case ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case ACT_SOFTSIGN: { float t = 1.f - fabsf(a); return t * t; }
+    case ACT_SIGMOID: return a * (1.f - a);
+    case ACT_ELU: return a > 0.f ? 1.f : a + 1.f;
+    case ACT_SELU: return a > 0.f ? SELU_SCALE : a + SELU_SCALE * SELU_ALPHA;
+    case ACT_SWISH: { float s = 1.f / (1.f + expf(-z)); return s * (1.f + z * (1.f - s)); }
+    case ACT_SOFTPLUS: return -expm1f(-a);
+    case ACT_LEAKY_RELU: return a > 0.f ? 1.f : 0.2f;
+    default: return 1.f;
+  }
+}
+
+// SpatialDropout2D keep test: counter hash of (seed, dropout ordinal, image, channel).
+// Restated bit-for-bit by oracle/keras_ref.py:dropout_hash.
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int drop_id, uint64_t image, uint32_t c) {
+  uint64_t x = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(1 + drop_id);
+  x ^= image * 0xBF58476D1CE4E5B9ull;
+  x ^= (uint64_t)c * 0xD6E8FEB86659FD93ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+
+struct Epi {
+  int act, drop, zslot;
+  uint32_t thr;
+  float keep;
+};
+
+struct Ctx {
+  const int* prog;
+  const float* params;
+  const float* params_t;
+  float* lds;
+  int T;
+  int64_t row0;     // first row of the tile (batch-local)
+  int64_t nrows;    // valid rows
+  int P;            // positions per image
+  int64_t img_off;  // global index of this launch's first image (dropout hash)
+  uint64_t seed;
+};
+
+__device__ __forceinline__ int slot_w(const Ctx& c, int s, int w) {
+  return c.prog[c.prog[H_SLOTS_OFF] + s * S_WORDS + w];
+}
+
+__device__ __forceinline__ Epi load_epi(const int* o) {
+  Epi e;
+  e.act = o[O_EACT];
+  e.drop = o[O_EDROP];
+  e.zslot = o[O_EZ];
+  e.thr = (uint32_t)o[O_ETHR];
+  e.keep = __int_as_float(o[O_EKEEP]);
+  return e;
+}
+
+__device__ __forceinline__ int64_t image_of(const Ctx& c, int r) {
+  return (c.row0 + r) / c.P + c.img_off;
+}
+
+__device__ __forceinline__ float epi_fwd(const Ctx& c, const Epi& e, float z, int r, int ch) {
+  float a = act_f(e.act, z);
+  if (e.drop >= 0) a = drop_hash(c.seed, e.drop, image_of(c, r), ch) >= e.thr ? a / e.keep : 0.f;
+  return a;
+}
+
+// gradient through the epilogue: g = dL/d(stored output), val = stored output
+__device__ __forceinline__ float epi_bwd(const Ctx& c, const Epi& e, float g, float val, float z,
+                                         int r, int ch) {
+  if (e.drop >= 0) {
+    if (drop_hash(c.seed, e.drop, image_of(c, r), ch) < e.thr) return 0.f;
+    g = g / e.keep;
+    val = val * e.keep;
+  }
+  return e.act == ACT_LINEAR ? g : g * act_grad(e.act, val, z);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+struct Args {
+  const int* prog;
+  const float* params;
+  const float* params_t;
+  const float* x;
+  const float* ytrue;
+  const int* idx;
+  float* y;          // forward output
+  float* ws;         // per-workgroup partials (train / eval)
+  int64_t nrows;
+  int P;
+  int64_t img_off;
+  float inv_count;
+  uint64_t seed;
+};
+
+// fused 2-layer regressor kernel (hpe_mlp2.hip)
+int mlp2_supported(const int* words);
+int mlp2_grid_cap(const int* words, int n_cu);
+int mlp2_launch(const int* words_host, const Args& a, int grid, hipStream_t s);

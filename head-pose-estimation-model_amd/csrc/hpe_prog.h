@@ -15,10 +15,12 @@ enum {
   H_MAGIC = 0, H_NOPS, H_NSLOTS, H_T, H_NW, H_IN_SLOT, H_OUT_SLOT, H_CIN, H_COUT,
   H_NPARAMS, H_NPARAMS_TRAIN, H_LDS_FLOATS, H_MAXACC, H_MAXTHIN, H_NTACC, H_OPS_OFF,
   H_SLOTS_OFF, H_BLK_OFF, H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB,
+  H_KIND,  // KIND_GENERIC: op list for rowprog_kernel; KIND_MLP2: one OP_MLP2 op for mlp2_kernel
   H_WORDS = 32
 };
 
 enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_EVAL = 2 };
+enum { KIND_GENERIC = 0, KIND_MLP2 = 1 };
 
 // ---- slot words: LDS float offset, channels, padded channels (even, %8), row stride -----------
 enum { S_OFF = 0, S_C, S_CP, S_STRIDE, S_WORDS = 4 };
@@ -43,7 +45,12 @@ enum {
   OP_DIN = 9,      // out (=|+=|epigrad) a . W^T                 MFMA
   OP_TDIN = 10,    // same, contraction N <= 8, VALU
   OP_EWB = 11,     // backward of OP_EW
-  OP_LNB = 12      // backward of OP_LN
+  OP_LNB = 12,     // backward of OP_LN
+  // fused 2-layer regressor (hpe_mlp2.hip): x (C_in) -> dense F (act1, dropout1) -> dense 3
+  // (act2, dropout2).  Fields: O_K C_in, O_N F, O_AUX3 N2 (=3), O_W W1, O_BIAS b1, O_AUX0 W2,
+  // O_AUX1 b2, O_E* layer-1 epilogue, O_AUX2 act2, O_TBASE drop2 id, O_TCOUNT drop2 threshold,
+  // O_F0 keep2, O_FLAGS row blocks per wave per tile (RBW), O_MODE column blocks (= waves).
+  OP_MLP2 = 13
 };
 
 enum { EW_HAS_B = 1, EW_MUL = 2, EW_AFFINE = 4 };             // OP_EW / OP_EWB flags

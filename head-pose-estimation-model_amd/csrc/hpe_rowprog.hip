@@ -28,119 +28,8 @@
 #include "hpe_prog.h"
 #include "../../include/hpe.h"
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+#include "hpe_common.h"
 
-#define MAXTHIN 4
-
-// ------------------------------------------------------------------------------------------------
-// activations and their derivatives (derivative from the stored output where possible)
-// ------------------------------------------------------------------------------------------------
-#define SELU_ALPHA 1.6732632423543772848170429916717f
-#define SELU_SCALE 1.0507009873554804934193349852946f
-
-__device__ __forceinline__ float act_f(int act, float z) {
-  switch (act) {
-    case ACT_TANH: return tanhf(z);
-    case ACT_RELU: return z > 0.f ? z : 0.f;
-    case ACT_SOFTSIGN: return z / (1.f + fabsf(z));
-    case ACT_SIGMOID: return 1.f / (1.f + expf(-z));
-    case ACT_ELU: return z > 0.f ? z : expm1f(z);
-    case ACT_SELU: return SELU_SCALE * (z > 0.f ? z : SELU_ALPHA * expm1f(z));
-    case ACT_SWISH: return z / (1.f + expf(-z));
-    case ACT_SOFTPLUS: return z > 20.f ? z : log1pf(expf(z));
-    case ACT_LEAKY_RELU: return z > 0.f ? z : 0.2f * z;
-    default: return z;
-  }
-}
-
-// d act / dz given a = act(z) (and z for swish)
-__device__ __forceinline__ float act_grad(int act, float a, float z) {
-  switch (act) {
-    case ACT_TANH: return 1.f - a * a;
-    case ACT_RELU: return a > 0.f ? 1.f : 0.f;
-    case ACT_SOFTSIGN: { float t = 1.f - fabsf(a); return t * t; }
-    case ACT_SIGMOID: return a * (1.f - a);
-    case ACT_ELU: return a > 0.f ? 1.f : a + 1.f;
-    case ACT_SELU: return a > 0.f ? SELU_SCALE : a + SELU_SCALE * SELU_ALPHA;
-    case ACT_SWISH: { float s = 1.f / (1.f + expf(-z)); return s * (1.f + z * (1.f - s)); }
-    case ACT_SOFTPLUS: return -expm1f(-a);
-    case ACT_LEAKY_RELU: return a > 0.f ? 1.f : 0.2f;
-    default: return 1.f;
-  }
-}
-
-// SpatialDropout2D keep test: counter hash of (seed, dropout ordinal, image, channel).
-// Restated bit-for-bit by oracle/keras_ref.py:dropout_hash.
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int drop_id, uint64_t image, uint32_t c) {
-  uint64_t x = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(1 + drop_id);
-  x ^= image * 0xBF58476D1CE4E5B9ull;
-  x ^= (uint64_t)c * 0xD6E8FEB86659FD93ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return (uint32_t)(x >> 32);
-}
-
-struct Epi {
-  int act, drop, zslot;
-  uint32_t thr;
-  float keep;
-};
-
-struct Ctx {
-  const int* prog;
-  const float* params;
-  const float* params_t;
-  float* lds;
-  int T;
-  int64_t row0;     // first row of the tile (batch-local)
-  int64_t nrows;    // valid rows
-  int P;            // positions per image
-  int64_t img_off;  // global index of this launch's first image (dropout hash)
-  uint64_t seed;
-};
-
-__device__ __forceinline__ int slot_w(const Ctx& c, int s, int w) {
-  return c.prog[c.prog[H_SLOTS_OFF] + s * S_WORDS + w];
-}
-
-__device__ __forceinline__ Epi load_epi(const int* o) {
-  Epi e;
-  e.act = o[O_EACT];
-  e.drop = o[O_EDROP];
-  e.zslot = o[O_EZ];
-  e.thr = (uint32_t)o[O_ETHR];
-  e.keep = __int_as_float(o[O_EKEEP]);
-  return e;
-}
-
-__device__ __forceinline__ int64_t image_of(const Ctx& c, int r) {
-  return (c.row0 + r) / c.P + c.img_off;
-}
-
-__device__ __forceinline__ float epi_fwd(const Ctx& c, const Epi& e, float z, int r, int ch) {
-  float a = act_f(e.act, z);
-  if (e.drop >= 0) a = drop_hash(c.seed, e.drop, image_of(c, r), ch) >= e.thr ? a / e.keep : 0.f;
-  return a;
-}
-
-// gradient through the epilogue: g = dL/d(stored output), val = stored output
-__device__ __forceinline__ float epi_bwd(const Ctx& c, const Epi& e, float g, float val, float z,
-                                         int r, int ch) {
-  if (e.drop >= 0) {
-    if (drop_hash(c.seed, e.drop, image_of(c, r), ch) < e.thr) return 0.f;
-    g = g / e.keep;
-    val = val * e.keep;
-  }
-  return e.act == ACT_LINEAR ? g : g * act_grad(e.act, val, z);
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 // ------------------------------------------------------------------------------------------------
 // OP_DENSE: out[r][n] = epi(sum_k a[r][k] W[k][n] + b[n]) on fp32 MFMA 32x32x2.
@@ -573,21 +462,7 @@ __device__ __forceinline__ void op_lnb(const Ctx& c, const int* o) {
 // ------------------------------------------------------------------------------------------------
 // the kernel
 // ------------------------------------------------------------------------------------------------
-struct Args {
-  const int* prog;
-  const float* params;
-  const float* params_t;
-  const float* x;
-  const float* ytrue;
-  const int* idx;
-  float* y;          // forward output
-  float* ws;         // per-workgroup partials (train / eval)
-  int64_t nrows;
-  int P;
-  int64_t img_off;
-  float inv_count;
-  uint64_t seed;
-};
+
 
 template <int NW, int MAXACC>
 __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
@@ -874,6 +749,7 @@ static int fail(int code, const char* fmt, ...) {
 struct hpe_program {
   int* dwords;
   int hdr[H_WORDS];
+  int* words;  // host copy (fused-kernel geometry)
   int n_cu;
   int grid_cap;
 };
@@ -905,12 +781,16 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   if (!words || !out || n_words < H_WORDS) return fail(HPE_EINVAL, "program: null or short word stream");
   if (words[H_MAGIC] != HPE_MAGIC) return fail(HPE_EINVAL, "program: bad magic");
   const int nw = words[H_NW], T = words[H_T];
+  const bool fused = words[H_KIND] == KIND_MLP2;
   if (T <= 0 || T % 32) return fail(HPE_EINVAL, "program: T=%d must be a positive multiple of 32", T);
-  if (!pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
+  if (fused && !mlp2_supported(words)) return fail(HPE_EINVAL, "program: unsupported fused 2-layer geometry");
+  if (!fused && !pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
   if (words[H_MAXTHIN] > MAXTHIN) return fail(HPE_EINVAL, "program: MAXTHIN=%d > %d", words[H_MAXTHIN], MAXTHIN);
   if ((int64_t)(words[H_LDS_FLOATS] + 32) * 4 > 160 * 1024) return fail(HPE_EINVAL, "program: LDS %d floats exceeds 160 KiB", words[H_LDS_FLOATS]);
   hpe_program* p = new hpe_program();
   memcpy(p->hdr, words, sizeof(p->hdr));
+  p->words = new int[n_words];
+  memcpy(p->words, words, n_words * sizeof(int32_t));
   hipError_t e = hipMalloc(&p->dwords, n_words * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
   e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
@@ -927,8 +807,12 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   if (words[H_WG_PER_CU] > 0 && per_cu > words[H_WG_PER_CU]) per_cu = words[H_WG_PER_CU];
   if (per_cu < 1) per_cu = 1;
   p->grid_cap = ncu * per_cu;
-  kfn_t k = pick_kernel(nw, words[H_MAXACC]);
-  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (words[H_LDS_FLOATS] + 32) * 4);
+  if (fused) {
+    p->grid_cap = mlp2_grid_cap(words, ncu);
+  } else {
+    kfn_t k = pick_kernel(nw, words[H_MAXACC]);
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (words[H_LDS_FLOATS] + 32) * 4);
+  }
   *out = p;
   return HPE_OK;
 }
@@ -936,6 +820,7 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
 extern "C" int hpe_program_destroy(hpe_program* p) {
   if (!p) return HPE_OK;
   hipFree(p->dwords);
+  delete[] p->words;
   delete p;
   return HPE_OK;
 }
@@ -953,8 +838,12 @@ extern "C" size_t hpe_workspace_size(const hpe_program* p, int64_t n_rows) {
 }
 
 static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
-  kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC]);
   const int grid = hpe_launch_grid(p, nrows);
+  if (p->hdr[H_KIND] == KIND_MLP2) {
+    if (mlp2_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "mlp2 launch: %s", hipGetErrorString(hipGetLastError()));
+    return HPE_OK;
+  }
+  kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC]);
   hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), (p->hdr[H_LDS_FLOATS] + 32) * 4, s, a);
   HIPCHK(hipGetLastError());
   return HPE_OK;

@@ -22,7 +22,7 @@ import numpy as np
 HPE_MAGIC = 0x31455048
 (H_MAGIC, H_NOPS, H_NSLOTS, H_T, H_NW, H_IN_SLOT, H_OUT_SLOT, H_CIN, H_COUT, H_NPARAMS,
  H_NPARAMS_TRAIN, H_LDS_FLOATS, H_MAXACC, H_MAXTHIN, H_NTACC, H_OPS_OFF, H_SLOTS_OFF, H_BLK_OFF,
- H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB) = range(24)
+ H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB, H_KIND) = range(25)
 H_WORDS = 32
 MODE_FWD, MODE_TRAIN, MODE_EVAL = 0, 1, 2
 S_WORDS = 4
@@ -30,7 +30,7 @@ S_WORDS = 4
  O_AUX0, O_AUX1, O_AUX2, O_AUX3, O_TBASE, O_TCOUNT, O_F0, O_F1, O_MODE, O_WSEL) = range(24)
 O_WORDS = 24
 (OP_DENSE, OP_TDENSE, OP_EW, OP_LN, OP_LOSS, OP_EPIGRAD, OP_DW, OP_TACC, OP_DIN, OP_TDIN, OP_EWB,
- OP_LNB) = range(1, 13)
+ OP_LNB, OP_MLP2) = range(1, 14)
 EW_HAS_B, EW_MUL, EW_AFFINE = 1, 2, 4
 DST_STORE, DST_ACCUM, DST_EPIGRAD = 0, 1, 2
 TACC_GEMM, TACC_BIAS, TACC_DIAG = 0, 1, 2
@@ -259,7 +259,7 @@ def _reg(cfg, key):
 
 
 def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_per_cu=0,
-                  trainable=None):
+                  trainable=None, fused=True, rbw=1):
     """Compile to a Program.  weights: dict key -> np.ndarray (Keras '<layer>/<var>' keys)."""
     modes = {'fwd': MODE_FWD, 'train': MODE_TRAIN, 'eval': MODE_EVAL}
     if mode not in modes:
@@ -355,7 +355,12 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
     b.fuse_epilogues()
     live = {x_t.id} | {f.out.id for f in b.fops}
     b.tensors = [t for t in b.tensors if t.id in live]
+    if fused:
+        mlp2 = _try_mlp2(b, x_t, y_t, modes[mode], n_train, l2c, P)
+        if mlp2 is not None:
+            return mlp2
     prog = _finish(b, x_t, y_t, modes[mode], training, P, T, NW, wg_per_cu, n_train, l2c)
+    prog.kind = 'generic'
     return prog
 
 
@@ -950,3 +955,84 @@ def _liveness(E, in_slot, out_slot, mode):
         rd(len(E.ops), out_slot)
     return [((first[s] if first[s] is not None else -1), max(last[s], first[s] if first[s] is not None else -1))
             for s in range(n)]
+
+
+MLP2_MAX_F = 384
+
+
+def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
+    """Recognise the reference's dominant 2-layer regressor (train_96.py:65-110 create_model,
+    train_88.py:66-158 / 226-253): x -> dense F (act, dropout) -> dense 3 (act, dropout), and
+    emit a KIND_MLP2 program for the fused kernel (csrc/hpe_mlp2.hip)."""
+    if len(b.fops) != 2:
+        return None
+    f1, f2 = b.fops
+    if f1.kind != 'dense' or f2.kind != 'dense' or f1.ins[0] is not x_t or f2.ins[0] is not f1.out:
+        return None
+    if f2.out is not y_t or len(f1.out.consumers) != 1 or f1.transposed or f2.transposed:
+        return None
+    cin, F, n2 = f1.K, f1.N, f2.N
+    if n2 != 3 or cin % 4 or (cin + 7) // 8 * 4 not in (44, 48) or F > MLP2_MAX_F or F < 1:
+        return None
+    if f1.act in NEEDS_Z or f2.act in NEEDS_Z:
+        return None
+    if f1.w[0] != 'p' or f2.w[0] != 'p':
+        return None
+
+    def ref(r):
+        if r is None:
+            return -1
+        return r[1] if r[0] == 'p' else n_train + r[1]
+    ncb = -(-F // 32)
+    op = [0] * O_WORDS
+    op[O_TYPE] = OP_MLP2
+    op[O_K], op[O_N], op[O_AUX3] = cin, F, n2
+    op[O_W], op[O_BIAS], op[O_AUX0], op[O_AUX1] = ref(f1.w), ref(f1.bias), ref(f2.w), ref(f2.bias)
+    op[O_EACT], op[O_EDROP], op[O_ETHR], op[O_EKEEP], op[O_EZ] = f1.act, -1, 0, _f2i(1.0), -1
+    if f1.drop_id >= 0 and mode == MODE_TRAIN:
+        op[O_EDROP], op[O_ETHR] = f1.drop_id, _u2i(dropout_threshold(f1.rate))
+        op[O_EKEEP] = _f2i(np.float32(1.0) - np.float32(f1.rate))
+    op[O_AUX2], op[O_TBASE], op[O_TCOUNT], op[O_F0] = f2.act, -1, 0, _f2i(1.0)
+    if f2.drop_id >= 0 and mode == MODE_TRAIN:
+        op[O_TBASE], op[O_TCOUNT] = f2.drop_id, _u2i(dropout_threshold(f2.rate))
+        op[O_F0] = _f2i(np.float32(1.0) - np.float32(f2.rate))
+    op[O_FLAGS], op[O_MODE] = rbw, ncb
+    T = 32 * rbw
+    hdr = [0] * H_WORDS
+    hdr[H_MAGIC] = HPE_MAGIC
+    hdr[H_NOPS] = 1
+    hdr[H_T] = T
+    hdr[H_NW] = ncb
+    hdr[H_CIN], hdr[H_COUT] = cin, 3
+    hdr[H_NPARAMS] = n_train + b.const_off
+    hdr[H_NPARAMS_TRAIN] = n_train
+    hdr[H_MAXACC] = 1
+    hdr[H_MAXTHIN] = 1
+    hdr[H_SLOTS_OFF] = H_WORDS
+    hdr[H_OPS_OFF] = H_WORDS
+    hdr[H_MODE] = mode
+    hdr[H_SLAB] = -(-(n_train + 4) // 4) * 4
+    hdr[H_KIND] = 1
+    words = np.asarray(hdr + op, dtype=np.int64)
+    words = ((words + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int32)
+    prog = Program()
+    prog.kind = 'mlp2'
+    prog.words = words
+    prog.n_params = n_train + b.const_off
+    prog.n_train = n_train
+    prog.param_index = {k: b.pidx[k] for k, _ in b.params}
+    prog.param_keys = [k for k, _ in b.params]
+    prog.consts = np.concatenate(b.consts).astype(np.float32) if b.consts else np.zeros(0, np.float32)
+    prog.l2 = np.concatenate(l2c).astype(np.float32) if l2c else np.zeros(0, np.float32)
+    prog.mirror = list(b.mirror)
+    prog.n_mirror = sum(k * n for _, k, n, _ in b.mirror)
+    tpos = np.full(n_train, -1, dtype=np.int32)
+    for (o, K, N, mo) in b.mirror:
+        if o < n_train:
+            idx = np.arange(K * N)
+            tpos[o + idx] = mo + (idx % N) * K + idx // N
+    prog.tpos = tpos
+    prog.T, prog.NW, prog.mode = T, ncb, mode
+    prog.C_in, prog.C_out = cin, 3
+    prog.info = {'kind': 'mlp2', 'F': F, 'waves': ncb}
+    return prog

@@ -55,14 +55,16 @@ class Engine:
     """Parameters live on the device as one flat fp32 vector in Keras trainable_weights order
     (+ inference constants), plus the transposed mirror the backward GEMMs read."""
 
-    def __init__(self, model_config, weights, device=None):
+    def __init__(self, model_config, weights, device=None, fused=None):
         if not torch.cuda.is_available():
             raise _lib.HPEError('hpe needs a ROCm GPU (MI355X / gfx950); torch.cuda is unavailable')
         self.device = torch.device(device or 'cuda')
         self.model_config = model_config
         self.weights = dict(weights)
         self.progs = {}
-        base = compile_graph(model_config, self.weights, mode='fwd')
+        import os
+        self.fused = (os.environ.get('HPE_FUSED', '1') != '0') if fused is None else fused
+        base = compile_graph(model_config, self.weights, mode='fwd', fused=False)
         self.layout = base
         flat = np.zeros(base.n_train, dtype=np.float32)
         for k, (o, shp) in base.param_index.items():
@@ -81,7 +83,7 @@ class Engine:
     def program(self, mode, P=1):
         key = (mode, P == 1)
         if key not in self.progs:
-            prog = compile_graph(self.model_config, self.weights, mode=mode, P=P)
+            prog = compile_graph(self.model_config, self.weights, mode=mode, P=P, fused=self.fused)
             if prog.n_train != self.n_train:
                 raise RuntimeError('parameter layout mismatch between programs')
             if prog.consts.size and self.params.numel() != self.n_train + prog.consts.size:
