@@ -270,6 +270,8 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
         raise ValueError('row programs need a single-output graph (got %d outputs)' % len(outs))
     order = _topo(layers, outs)
     b = _Builder(weights, mode, P, trainable)
+    b.drop_ids = {l['name']: i for i, l in enumerate(
+        [l for l in layers if l['class_name'] in ('SpatialDropout2D', 'Dropout')])}
 
     # parameter layout: trainable weights in Keras trainable_weights order (layer order, kernel
     # before bias; MHA query/key/value/output) -- the same flat order the optimizer state uses.
@@ -451,8 +453,7 @@ def _lower(b, l, tmap, training, P):
         if not 0.0 <= rate <= 1.0:
             raise ValueError('Invalid value %s received for `rate`, expected a value between 0 '
                              'and 1.' % rate)
-        did = b.drop_count
-        b.drop_count += 1
+        did = b.drop_ids[name]   # ordinal in model_config layer order (oracle numbering)
         if not training or rate == 0.0:
             return alias()
         t = b.tensor(x.C, name)

@@ -20,6 +20,7 @@ from . import layers as L
 from . import optimizers as O
 from . import random as hrandom
 from .callbacks import Callback, History
+from .parallel import all_reduce_grad, batch_slice
 
 KERAS_VERSION = '2.13.1'
 
@@ -259,9 +260,7 @@ class Model:
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0
                 nbs.append(nb)
-                # this rank's contiguous slice of the global batch
-                r0 = b0 + (nb * rank) // world
-                r1 = b0 + (nb * (rank + 1)) // world
+                r0, r1 = batch_slice(b0, b1, rank, world)   # this rank's share of the batch
                 seed = hrandom.dropout_seed(eng.iterations + 1)
                 if r1 > r0:
                     eng.gradient(xd, yd, P, idx[r0:r1], r1 - r0, 1.0 / (nb * P * 3), seed,
@@ -269,8 +268,7 @@ class Model:
                 else:
                     eng.grad.zero_()
                 if world > 1:
-                    dist, grp = self._dist
-                    dist.all_reduce(eng.grad, group=grp)
+                    all_reduce_grad(eng.grad, self._dist[1])
                 eng.optimizer_step(self.optimizer, stats[s])
             st = stats.cpu().numpy().astype(np.float64)
             nbs = np.asarray(nbs, dtype=np.float64)
