@@ -207,7 +207,8 @@ def main():
             'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': PEAK_FP32 / 1e12,
                          'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32,
                          'traffic': _traffic('train'),
-                         'kernel': 'rowprog_kernel<12,4> + reduce_kernel (hpe_train_step + hpe_reduce)',
+                         'kernel': {'mlp2': 'mlp2_kernel', 'generic': 'rowprog_kernel'}.get(
+                             eng.program('train', P).prog.kind, '?') + ' + reduce_kernel (hpe_train_step + hpe_reduce)',
                          'kernel_ms': train_ms, 'flop_per_launch': flop_launch},
             'train_mse_last_step': loss_mse,
         }
@@ -246,7 +247,9 @@ def main():
             'roofline': {'bound': 'hbm', 'achieved': bytes_launch / (ims * 1e-3) / 1e9,
                          'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
                          'frac': bytes_launch / (ims * 1e-3) / PEAK_HBM,
-                         'traffic': _traffic('infer'), 'kernel': 'rowprog_kernel<4,1> (hpe_forward)',
+                         'traffic': _traffic('infer'),
+                         'kernel': {'chain': 'chain_fwd_kernel', 'generic': 'rowprog_kernel'}.get(
+                             ie.program('fwd', P).prog.kind, '?') + ' (hpe_forward)',
                          'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
                          'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
     if rank == 0 and world == 1 and not a.no_cpu:

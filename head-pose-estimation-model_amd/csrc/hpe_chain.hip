@@ -1,0 +1,200 @@
+// hpe_chain.hip — fused forward of the narrow regressor chains (inference / predict / evaluate):
+//   x (88|96 ch) -> dense F1 <= 32 (act1) [-> dense F2 <= 32 (act2)] -> dense 3 (act3)
+// e.g. the selected Model-96 head hrchr82r (96-32-16-3 tanh, blazeFaceDetectorH5.py:102) and the
+// create_model(F <= 32) checkpoints.  This is the HBM-bound kernel of the path (18 FLOP/B): every
+// wave streams its own 32-row tiles HBM -> LDS with global_load_lds (no VGPR staging, no
+// workgroup barrier in the loop) and keeps every weight it needs in registers:
+//   layer 1: Z1^T = W1^T . X^T on v_mfma_f32_32x32x2_f32 (A = W1 columns in VGPRs, B = X rows from
+//            LDS, XOR-swizzled 16-B chunks -> conflict-free ds_read_b128), hidden unit n in the
+//            accumulator registers, the row on the lane;
+//   layer 2: Z2^T = W2^T . A1^T consumes A1^T straight from the accumulator registers as the MFMA
+//            B operand (contraction over the register index: no LDS round trip);
+//   layer 3: 3-wide head on the VALU (per-lane dot products, one cross-half add), 12 B per row out.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hpe_common.h"
+
+#define CHAIN_NW 12                     // waves per workgroup (3 per SIMD)
+#define CHAIN_KH 48                     // rows of 24 16-B chunks: 88- or 96-channel inputs
+#define CHAIN_XF (32 * CHAIN_KH * 2)    // floats per wave X tile
+#define CHAIN_TAB 1280                  // floats of shared weight tables per workgroup
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __forceinline__ int csw(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+__device__ __forceinline__ float ctanh(float z) {
+  const float t = __expf(-2.f * fabsf(z));
+  return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), z);
+}
+
+// A >= 0: activation fixed at compile time (the common tanh-tanh-linear heads); A < 0: read from the op
+template <int A>
+__device__ __forceinline__ float cact(int act, float z) {
+  const int a = A >= 0 ? A : act;
+  if (A >= 0 && a == ACT_TANH) return ctanh(z);
+  if (A >= 0 && a == ACT_LINEAR) return z;
+  return act_f(a, z);
+}
+
+// op fields: O_K C_in, O_N F1, O_AUX3 F2 (0 = no middle layer), O_W W1, O_BIAS b1, O_AUX0 W2,
+// O_AUX1 b2, O_AUX2 W3, O_TBASE b3, O_EACT act1, O_FLAGS act2, O_MODE act3, O_TCOUNT N3 (= 3)
+template <int A1, int A2, int A3, int GATHER>
+__global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int* prog = args.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int Cin = o[O_K], F1 = o[O_N], F2 = o[O_AUX3];
+  const int act1 = o[O_EACT], act2 = o[O_FLAGS], act3 = o[O_MODE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const float* P_ = args.params;
+  // shared tables: W2^T-ready [32][32] (row n, col m), b1[32], b2[32], W3 rows padded to 4 [32][4], b3[4]
+  float* tw2 = lds;
+  float* tb1 = tw2 + 1024;
+  float* tb2 = tb1 + 32;
+  float* tw3 = tb2 + 32;     // 128
+  float* tb3 = tw3 + 128;    // 4
+  float* xs = lds + CHAIN_TAB + wave * CHAIN_XF;
+  const int Fh = F2 > 0 ? F2 : F1;   // width feeding the 3-wide head
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+    const int nn = i >> 5, m = i & 31;
+    tw2[i] = (F2 > 0 && nn < F1 && m < F2) ? P_[o[O_AUX0] + nn * F2 + m] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) {
+    tb1[i] = (i < F1 && o[O_BIAS] >= 0) ? P_[o[O_BIAS] + i] : 0.f;
+    tb2[i] = (F2 > 0 && i < F2 && o[O_AUX1] >= 0) ? P_[o[O_AUX1] + i] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    const int nn = i >> 2, j = i & 3;
+    tw3[i] = (nn < Fh && j < 3) ? P_[o[O_AUX2] + nn * 3 + j] : 0.f;
+  }
+  if (threadIdx.x < 4) tb3[threadIdx.x] = (threadIdx.x < 3 && o[O_TBASE] >= 0) ? P_[o[O_TBASE] + threadIdx.x] : 0.f;
+
+  // W1 column n = l32 as the A operand: k = half*48 + m
+  float w1[CHAIN_KH];
+#pragma unroll
+  for (int m = 0; m < CHAIN_KH; ++m) {
+    const int k = half * CHAIN_KH + m;
+    const float v = P_[o[O_W] + (size_t)min(k, Cin - 1) * F1 + min(l32, F1 - 1)];
+    w1[m] = (k < Cin && l32 < F1) ? v : 0.f;
+  }
+  __syncthreads();
+  // per-lane views of the tables (register g <-> hidden unit R(g) + 4*half)
+  float b1r[16], w2r[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int nn = (g & 3) + 8 * (g >> 2) + 4 * half;
+    b1r[g] = tb1[nn];
+    w2r[g] = tw2[nn * 32 + l32];     // A of layer 2: W2^T[i = m = l32][k <-> n]
+  }
+
+  const int64_t nrows = args.nrows;
+  const int64_t ntiles = (nrows + 31) / 32;
+  const int P = args.P;
+  const int64_t gw = (int64_t)blockIdx.x * CHAIN_NW + wave;
+  const int64_t nw = (int64_t)gridDim.x * CHAIN_NW;
+  for (int64_t tile = gw; tile < ntiles; tile += nw) {
+    const int64_t row0 = tile * 32;
+    // ---- HBM -> this wave's LDS tile: 12 x 1 KiB global_load_lds, swizzled source chunks ----
+    // per-lane (row, chunk) of each piece is recomputed per tile from an opaque lane id (cheap VALU)
+    // instead of being hoisted into 24+ loop-carried VGPRs; the tile base is wave-uniform (SGPRs).
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
+    const float* xt = args.x + row0 * Cin;
+#pragma unroll
+    for (int pc = 0; pc < 12; ++pc) {
+      const int slot = pc * 64 + lz;
+      const int r = slot / 24, ph = slot - r * 24;
+      const int c = csw(r, ph);
+      const int cc = 4 * c < Cin ? c : 0;
+      const int rr = min(r, last);
+      const float* src;
+      if (GATHER) {
+        const int64_t R = row0 + rr;
+        const int64_t img = R / P, pos = R - img * P;
+        src = args.x + ((int64_t)args.idx[img] * P + pos) * Cin + 4 * cc;
+      } else {
+        src = xt + (rr * Cin + 4 * cc);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + pc * 256), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- layer 1 ----
+    const float* xr = xs + l32 * 96;
+    const int sw = (l32 >> 1) & 7;
+    f32x16 acc = {};
+#pragma unroll
+    for (int m = 0; m < CHAIN_KH; m += 4) {
+      const f32x4 a = *(const f32x4*)(xr + 4 * ((half * 12 + m / 4) ^ sw));
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[m + 0], a.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[m + 1], a.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[m + 2], a.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[m + 3], a.w, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, acc[g] + b1r[g]);
+    // loop-invariant LDS tables are re-read per tile (an opaque zero offset keeps the compiler from
+    // hoisting 64 more VGPRs of them out of the loop; the reads are broadcast / conflict-free)
+    int toff = 0;
+    asm volatile("" : "+v"(toff));
+    // ---- layer 2 (optional) ----
+    f32x16 h = acc;
+    if (F2 > 0) {
+      f32x16 acc2 = {};
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2r[g], acc[g], acc2, 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
+        acc2[g] = cact<A2>(act2, acc2[g] + tb2[toff + mm]);
+      }
+      h = acc2;
+    }
+    // ---- 3-wide head: per-lane partial over its 16 units, then the other half's ----
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int nn = (g & 3) + 8 * (g >> 2) + 4 * half;
+      const f32x4 w = *(const f32x4*)(tw3 + toff + nn * 4);
+      s0 = fmaf(h[g], w.x, s0);
+      s1 = fmaf(h[g], w.y, s1);
+      s2 = fmaf(h[g], w.z, s2);
+    }
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const int64_t R = row0 + l32;
+    if (half == 0 && R < nrows) {
+      float* yp = args.y + R * 3;
+      yp[0] = cact<A3>(act3, s0 + tb3[0]);
+      yp[1] = cact<A3>(act3, s1 + tb3[1]);
+      yp[2] = cact<A3>(act3, s2 + tb3[2]);
+    }
+  }
+}
+
+typedef void (*chain_fn)(Args);
+
+int chain_supported(const int* w) {
+  const int* o = w + w[H_OPS_OFF];
+  return o[O_K] > 80 && o[O_K] <= 96 && (o[O_K] & 3) == 0 && o[O_N] >= 1 && o[O_N] <= 32 &&
+         o[O_AUX3] >= 0 && o[O_AUX3] <= 32 && o[O_TCOUNT] == 3;
+}
+
+int chain_lds_bytes() { return (CHAIN_TAB + CHAIN_NW * CHAIN_XF) * 4; }
+
+int chain_grid_cap(int n_cu) { return n_cu; }  // one 12-wave workgroup per CU (LDS ~149 KiB)
+
+int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
+  const int* o = w + w[H_OPS_OFF];
+  const bool tt_l = o[O_EACT] == ACT_TANH && (o[O_AUX3] == 0 || o[O_FLAGS] == ACT_TANH) && o[O_MODE] == ACT_LINEAR;
+  chain_fn k = tt_l ? (a.idx ? chain_fwd_kernel<ACT_TANH, ACT_TANH, ACT_LINEAR, 1>
+                             : chain_fwd_kernel<ACT_TANH, ACT_TANH, ACT_LINEAR, 0>)
+                    : (a.idx ? chain_fwd_kernel<-1, -1, -1, 1> : chain_fwd_kernel<-1, -1, -1, 0>);
+  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, chain_lds_bytes());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CHAIN_NW * 64), chain_lds_bytes(), s, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -139,3 +139,9 @@ struct Args {
 int mlp2_supported(const int* words);
 int mlp2_grid_cap(const int* words, int n_cu);
 int mlp2_launch(const int* words_host, const Args& a, int grid, hipStream_t s);
+
+// fused narrow chain forward (hpe_chain.hip)
+int chain_supported(const int* words);
+int chain_grid_cap(int n_cu);
+int chain_lds_bytes();
+int chain_launch(const int* words_host, const Args& a, int grid, hipStream_t s);

@@ -20,7 +20,7 @@ enum {
 };
 
 enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_EVAL = 2 };
-enum { KIND_GENERIC = 0, KIND_MLP2 = 1 };
+enum { KIND_GENERIC = 0, KIND_MLP2 = 1, KIND_CHAIN = 2 };
 
 // ---- slot words: LDS float offset, channels, padded channels (even, %8), row stride -----------
 enum { S_OFF = 0, S_C, S_CP, S_STRIDE, S_WORDS = 4 };
@@ -50,7 +50,11 @@ enum {
   // (act2, dropout2).  Fields: O_K C_in, O_N F, O_AUX3 N2 (=3), O_W W1, O_BIAS b1, O_AUX0 W2,
   // O_AUX1 b2, O_E* layer-1 epilogue, O_AUX2 act2, O_TBASE drop2 id, O_TCOUNT drop2 threshold,
   // O_F0 keep2, O_FLAGS row blocks per wave per tile (RBW), O_MODE column blocks (= waves).
-  OP_MLP2 = 13
+  OP_MLP2 = 13,
+  // fused narrow chain forward (hpe_chain.hip): x -> dense F1 <= 32 -> [dense F2 <= 32] -> dense 3.
+  // Fields: O_K C_in, O_N F1, O_AUX3 F2 (0 = none), O_W W1, O_BIAS b1, O_AUX0 W2, O_AUX1 b2,
+  // O_AUX2 W3, O_TBASE b3, O_EACT act1, O_FLAGS act2, O_MODE act3, O_TCOUNT 3.
+  OP_CHAIN = 14
 };
 
 enum { EW_HAS_B = 1, EW_MUL = 2, EW_AFFINE = 4 };             // OP_EW / OP_EWB flags

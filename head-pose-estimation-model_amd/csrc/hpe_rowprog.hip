@@ -781,10 +781,13 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   if (!words || !out || n_words < H_WORDS) return fail(HPE_EINVAL, "program: null or short word stream");
   if (words[H_MAGIC] != HPE_MAGIC) return fail(HPE_EINVAL, "program: bad magic");
   const int nw = words[H_NW], T = words[H_T];
-  const bool fused = words[H_KIND] == KIND_MLP2;
+  const int kind = words[H_KIND];
+  const bool fused = kind == KIND_MLP2;
   if (T <= 0 || T % 32) return fail(HPE_EINVAL, "program: T=%d must be a positive multiple of 32", T);
   if (fused && !mlp2_supported(words)) return fail(HPE_EINVAL, "program: unsupported fused 2-layer geometry");
-  if (!fused && !pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
+  if (kind == KIND_CHAIN && (!chain_supported(words) || words[H_MODE] != MODE_FWD))
+    return fail(HPE_EINVAL, "program: unsupported fused chain geometry");
+  if (kind == KIND_GENERIC && !pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
   if (words[H_MAXTHIN] > MAXTHIN) return fail(HPE_EINVAL, "program: MAXTHIN=%d > %d", words[H_MAXTHIN], MAXTHIN);
   if ((int64_t)(words[H_LDS_FLOATS] + 32) * 4 > 160 * 1024) return fail(HPE_EINVAL, "program: LDS %d floats exceeds 160 KiB", words[H_LDS_FLOATS]);
   hpe_program* p = new hpe_program();
@@ -809,6 +812,8 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   p->grid_cap = ncu * per_cu;
   if (fused) {
     p->grid_cap = mlp2_grid_cap(words, ncu);
+  } else if (kind == KIND_CHAIN) {
+    p->grid_cap = chain_grid_cap(ncu);
   } else {
     kfn_t k = pick_kernel(nw, words[H_MAXACC]);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (words[H_LDS_FLOATS] + 32) * 4);
@@ -827,7 +832,8 @@ extern "C" int hpe_program_destroy(hpe_program* p) {
 
 extern "C" int hpe_launch_grid(const hpe_program* p, int64_t n_rows) {
   if (!p) return 0;
-  const int64_t ntiles = (n_rows + p->hdr[H_T] - 1) / p->hdr[H_T];
+  int64_t ntiles = (n_rows + p->hdr[H_T] - 1) / p->hdr[H_T];
+  if (p->hdr[H_KIND] == KIND_CHAIN) ntiles = (ntiles + p->hdr[H_NW] - 1) / p->hdr[H_NW];  // per-wave tiles
   int64_t g = ntiles < p->grid_cap ? ntiles : p->grid_cap;
   return (int)(g < 1 ? 1 : g);
 }
@@ -841,6 +847,10 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   const int grid = hpe_launch_grid(p, nrows);
   if (p->hdr[H_KIND] == KIND_MLP2) {
     if (mlp2_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "mlp2 launch: %s", hipGetErrorString(hipGetLastError()));
+    return HPE_OK;
+  }
+  if (p->hdr[H_KIND] == KIND_CHAIN) {
+    if (chain_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "chain launch: %s", hipGetErrorString(hipGetLastError()));
     return HPE_OK;
   }
   kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC]);

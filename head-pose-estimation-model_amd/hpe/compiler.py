@@ -30,7 +30,7 @@ S_WORDS = 4
  O_AUX0, O_AUX1, O_AUX2, O_AUX3, O_TBASE, O_TCOUNT, O_F0, O_F1, O_MODE, O_WSEL) = range(24)
 O_WORDS = 24
 (OP_DENSE, OP_TDENSE, OP_EW, OP_LN, OP_LOSS, OP_EPIGRAD, OP_DW, OP_TACC, OP_DIN, OP_TDIN, OP_EWB,
- OP_LNB, OP_MLP2) = range(1, 14)
+ OP_LNB, OP_MLP2, OP_CHAIN) = range(1, 15)
 EW_HAS_B, EW_MUL, EW_AFFINE = 1, 2, 4
 DST_STORE, DST_ACCUM, DST_EPIGRAD = 0, 1, 2
 TACC_GEMM, TACC_BIAS, TACC_DIAG = 0, 1, 2
@@ -358,6 +358,10 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
     live = {x_t.id} | {f.out.id for f in b.fops}
     b.tensors = [t for t in b.tensors if t.id in live]
     if fused:
+        if mode == 'fwd':
+            ch = _try_chain(b, x_t, y_t, n_train, l2c)
+            if ch is not None:
+                return ch
         mlp2 = _try_mlp2(b, x_t, y_t, modes[mode], n_train, l2c, P)
         if mlp2 is not None:
             return mlp2
@@ -998,12 +1002,16 @@ def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
         op[O_TBASE], op[O_TCOUNT] = f2.drop_id, _u2i(dropout_threshold(f2.rate))
         op[O_F0] = _f2i(np.float32(1.0) - np.float32(f2.rate))
     op[O_FLAGS], op[O_MODE] = rbw, ncb
-    T = 32 * rbw
+    return _fused_program(b, op, 1, 32 * rbw, ncb, mode, n_train, l2c, cin,
+                          {'kind': 'mlp2', 'F': F, 'waves': ncb})
+
+
+def _fused_program(b, op, kind, T, nw, mode, n_train, l2c, cin, info):
     hdr = [0] * H_WORDS
     hdr[H_MAGIC] = HPE_MAGIC
     hdr[H_NOPS] = 1
     hdr[H_T] = T
-    hdr[H_NW] = ncb
+    hdr[H_NW] = nw
     hdr[H_CIN], hdr[H_COUT] = cin, 3
     hdr[H_NPARAMS] = n_train + b.const_off
     hdr[H_NPARAMS_TRAIN] = n_train
@@ -1013,11 +1021,11 @@ def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
     hdr[H_OPS_OFF] = H_WORDS
     hdr[H_MODE] = mode
     hdr[H_SLAB] = -(-(n_train + 4) // 4) * 4
-    hdr[H_KIND] = 1
+    hdr[H_KIND] = kind
     words = np.asarray(hdr + op, dtype=np.int64)
     words = ((words + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int32)
     prog = Program()
-    prog.kind = 'mlp2'
+    prog.kind = info['kind']
     prog.words = words
     prog.n_params = n_train + b.const_off
     prog.n_train = n_train
@@ -1033,7 +1041,43 @@ def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
             idx = np.arange(K * N)
             tpos[o + idx] = mo + (idx % N) * K + idx // N
     prog.tpos = tpos
-    prog.T, prog.NW, prog.mode = T, ncb, mode
+    prog.T, prog.NW, prog.mode = T, nw, mode
     prog.C_in, prog.C_out = cin, 3
-    prog.info = {'kind': 'mlp2', 'F': F, 'waves': ncb}
+    prog.info = info
     return prog
+
+
+def _try_chain(b, x_t, y_t, n_train, l2c):
+    """Inference chain x -> dense F1 <= 32 -> [dense F2 <= 32] -> dense 3 (e.g. hrchr82r
+    96-32-16-3, the selected Model-96 head): KIND_CHAIN program for csrc/hpe_chain.hip."""
+    f = b.fops
+    if len(f) not in (2, 3) or any(x.kind != 'dense' or x.transposed or x.drop_id >= 0 for x in f):
+        return None
+    if f[0].ins[0] is not x_t or f[-1].out is not y_t or f[-1].N != 3:
+        return None
+    for a, c in zip(f, f[1:]):
+        if c.ins[0] is not a.out or len(a.out.consumers) != 1:
+            return None
+    cin = f[0].K
+    if cin % 4 or not 80 < cin <= 96 or f[0].N > 32 or (len(f) == 3 and f[1].N > 32):
+        return None
+    if any(x.act in NEEDS_Z for x in f) or any(x.w[0] != 'p' for x in f):
+        return None
+
+    def ref(r):
+        if r is None:
+            return -1
+        return r[1] if r[0] == 'p' else n_train + r[1]
+    op = [0] * O_WORDS
+    op[O_TYPE] = OP_CHAIN
+    op[O_K], op[O_N] = cin, f[0].N
+    op[O_W], op[O_BIAS] = ref(f[0].w), ref(f[0].bias)
+    op[O_EACT] = f[0].act
+    if len(f) == 3:
+        op[O_AUX3], op[O_AUX0], op[O_AUX1], op[O_FLAGS] = f[1].N, ref(f[1].w), ref(f[1].bias), f[1].act
+    else:
+        op[O_AUX3], op[O_AUX0], op[O_AUX1], op[O_FLAGS] = 0, -1, -1, 0
+    op[O_AUX2], op[O_TBASE], op[O_MODE], op[O_TCOUNT] = ref(f[-1].w), ref(f[-1].bias), f[-1].act, 3
+    op[O_EDROP], op[O_EZ] = -1, -1
+    return _fused_program(b, op, 2, 32, 12, MODE_FWD, n_train, l2c, cin,
+                          {'kind': 'chain', 'widths': [x.N for x in f]})

@@ -235,3 +235,25 @@ def run(prog, params, x_rows, P=1, y_img=None, inv_count=1.0, seed=0, img_off=0)
         else:
             raise ValueError('op %d' % t)
     return {'out': S[int(hdr[C.H_OUT_SLOT])], 'grad': grad, 'sse': sse, 'sae': sae}
+
+
+def run_chain(prog, params, x_rows):
+    """KIND_CHAIN program (csrc/hpe_chain.hip): x -> dense F1 -> [dense F2] -> dense 3, from the op
+    words alone (field map in csrc/hpe_prog.h OP_CHAIN)."""
+    w = prog.words.astype(np.int64)
+    o = w[int(w[C.H_OPS_OFF]):]
+    assert int(o[C.O_TYPE]) == C.OP_CHAIN
+    p = np.asarray(params, dtype=np.float64)
+    cin, f1, f2 = int(o[C.O_K]), int(o[C.O_N]), int(o[C.O_AUX3])
+
+    def dense(x, wo, bo, k, n, act):
+        z = x @ p[wo:wo + k * n].reshape(k, n)
+        if bo >= 0:
+            z = z + p[bo:bo + n]
+        return _act(act, z)
+    h = dense(np.asarray(x_rows, np.float64), int(o[C.O_W]), int(o[C.O_BIAS]), cin, f1, int(o[C.O_EACT]))
+    fh = f1
+    if f2 > 0:
+        h = dense(h, int(o[C.O_AUX0]), int(o[C.O_AUX1]), f1, f2, int(o[C.O_FLAGS]))
+        fh = f2
+    return dense(h, int(o[C.O_AUX2]), int(o[C.O_TBASE]), fh, int(o[C.O_TCOUNT]), int(o[C.O_MODE]))

@@ -7,7 +7,7 @@ import pytest
 import hpe.compiler as C
 import rowprog_emu as EMU
 from oracle import keras_ref as K
-from util import fixture, index, input_channels
+from util import features, fixture, index, input_channels
 
 IDS = sorted(r for r in index() if not r.startswith('reg1'))
 
@@ -54,8 +54,30 @@ def test_fused_recognition():
         mc, w = fixture(rid)
         kinds[rid] = C.compile_graph(mc, w, 'fwd').kind
     assert kinds['sqnu665j'] == 'mlp2' and kinds['stoqa9pt'] == 'mlp2'
-    assert kinds['hrchr82r'] == 'generic' and kinds['ker7z9mv'] == 'generic'
+    assert kinds['hrchr82r'] == 'chain' and kinds['ker7z9mv'] == 'generic'
     assert sum(v == 'mlp2' for v in kinds.values()) >= 10
+    assert sum(v == 'chain' for v in kinds.values()) >= 20
+    assert C.compile_graph(*fixture('hrchr82r'), 'train').kind == 'generic'   # chain is forward-only
+
+
+def test_chain_words_emulated():
+    """The KIND_CHAIN op words (field map of csrc/hpe_prog.h OP_CHAIN) reproduce the oracle."""
+    n = 0
+    for rid in IDS:
+        mc, w = fixture(rid)
+        prog = C.compile_graph(mc, w, 'fwd')
+        if prog.kind != 'chain':
+            continue
+        n += 1
+        c = input_channels(mc)
+        x = features(64, c, seed=n)
+        flat = np.zeros(prog.n_train, np.float32)
+        for k, (o, shp) in prog.param_index.items():
+            flat[o:o + int(np.prod(shp))] = np.asarray(w[k], np.float32).ravel()
+        got = EMU.run_chain(prog, np.concatenate([flat, prog.consts]), x.reshape(-1, c))
+        ref = K.Graph(mc, w).forward(x).detach().numpy().reshape(-1, 3)
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4, err_msg=rid)
+    assert n >= 20
 
 
 def test_spatial_graph_rejects_non_row_local():

@@ -136,3 +136,29 @@ def test_evaluate_matches_oracle():
     ref_mse = float(np.mean((p - y) ** 2)) + float(g.regularization().item())
     assert abs(loss - ref_mse) <= 1e-4 * ref_mse
     assert abs(mae - float(np.mean(np.abs(p - y)))) <= 1e-4
+
+
+@pytest.mark.parametrize('rid', ['hrchr82r', 'fsjbki8r', '0klags84'])
+def test_chain_forward_ragged_and_gather(rid):
+    """Fused chain forward (csrc/hpe_chain.hip): ragged tails (n % 32 != 0), several tiles per wave
+    (n >> 32 x 12 waves x 256 CUs) and the image-index gather at P = 1 and P = 4."""
+    from hpe.engine import Engine
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    eng = Engine(mc, w)
+    assert eng.program('fwd', 1).prog.kind == 'chain'
+    g = K.Graph(mc, w)
+    for n in (1, 31, 33, 385, 100_003, 400_001):
+        x = features(n, c, seed=n)
+        ref = g.forward(x).detach().numpy().reshape(-1, 3)
+        got = eng.forward(torch.from_numpy(x.reshape(n, c)).cuda(), 1).cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL, err_msg='n=%d' % n)
+    flat = any(l['class_name'] == 'Flatten' for l in mc['config']['layers'])
+    for P in ((1,) if flat else (1, 4)):     # Flatten heads are row-local only at P == 1
+        n_img = 777
+        x = features(n_img, c, seed=P, h=1, w=P)
+        idx = np.random.default_rng(P).permutation(n_img)[:301].astype(np.int32)
+        ref = g.forward(x[idx]).detach().numpy().reshape(-1, 3)
+        got = eng.forward(torch.from_numpy(x.reshape(-1, c)).cuda(), P,
+                          idx=torch.from_numpy(idx).cuda()).cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL, err_msg='P=%d' % P)
