@@ -145,3 +145,6 @@ int chain_supported(const int* words);
 int chain_grid_cap(int n_cu);
 int chain_lds_bytes();
 int chain_launch(const int* words_host, const Args& a, int grid, hipStream_t s);
+
+// thread-local error message of the C ABI (hpe_last_error); returns code
+int hpe_fail(int code, const char* fmt, ...);

@@ -65,3 +65,21 @@ enum {
   ACT_LINEAR = 0, ACT_TANH, ACT_RELU, ACT_SOFTSIGN, ACT_SIGMOID, ACT_ELU, ACT_SELU, ACT_SWISH,
   ACT_SOFTPLUS, ACT_LEAKY_RELU
 };
+
+// ------------------------------------------------------------------------------------------------
+// BlazeFace backbone plan (csrc/hpe_blaze.hip; built by hpe/blazeface.py from the unified model's
+// model_config).  Header of BFH_WORDS, then n_ops ops of BFO_WORDS.  Activations between ops are
+// NHWC fp32 with the channel stride padded to a multiple of 8 (pad channels hold zeros).
+// ------------------------------------------------------------------------------------------------
+#define HPE_BF_MAGIC 0x46425048  // "HPBF"
+enum { BFH_MAGIC = 0, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF, BFH_WORDS = 8 };
+enum { BF_STEM = 1, BF_BLOCK = 2 };
+enum { BF_RES_NONE = 0, BF_RES_ID = 1, BF_RES_MAXPOOL = 2 };
+// buffers: image input, two ping-pong activations, then the six caller outputs
+enum { BF_BUF_IMG = 0, BF_BUF_A = 1, BF_BUF_B = 2, BF_BUF_OUT0 = 3, BF_NBUF = 9 };
+enum {
+  BFO_KIND = 0, BFO_H, BFO_W, BFO_HO, BFO_WO, BFO_CIN, BFO_COUT, BFO_CINP, BFO_COUTP,
+  BFO_STRIDE, BFO_PADT, BFO_PADL, BFO_DW, BFO_RES, BFO_RELU, BFO_SRC, BFO_DST, BFO_DST2,
+  BFO_SPLIT, BFO_TH, BFO_NI, BFO_DWW, BFO_PWW, BFO_PWB, BFO_CS, BFO_KS, BFO_ROWS, BFO_COLS,
+  BFO_NC, BFO_LDS, BFO_WORDS = 32
+};

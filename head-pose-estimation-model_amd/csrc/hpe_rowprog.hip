@@ -732,13 +732,14 @@ __global__ void optim_kernel(int kind, float lr, float alpha, float b1, float b2
 // ------------------------------------------------------------------------------------------------
 static thread_local char g_err[512];
 
-static int fail(int code, const char* fmt, ...) {
+int hpe_fail(int code, const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof g_err, fmt, ap);
   va_end(ap);
   return code;
 }
+#define fail hpe_fail
 
 #define HIPCHK(x)                                                                      \
   do {                                                                                 \
