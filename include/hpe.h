@@ -94,6 +94,26 @@ int hpe_optim_step(int32_t kind, float lr, float beta_1, float beta_2, float eps
 /* Blocks hpe_optim_step launches (stats holds 2 + this many floats). */
 int hpe_optim_grid(int64_t n);
 
+/* ---------------------------------------------------------------------------------------------
+ * BlazeFace backbone — replaces the TF call on the fused BlazeFace+regressor
+ * graph, `self.model.predict(...)` at BlazePoser/blazeFaceDetectorH5.py:272, for a whole batch.
+ * words: the plan hpe/blazeface.py builds from the unified model's model_config (csrc/hpe_prog.h
+ * BFH_* / BFO_*); params: the plan's flat fp32 parameter vector (device).
+ * images: (n_images, 128, 128, 3) NHWC fp32 in [-1, 1] (the detector's preprocessed input).
+ * outs: six device pointers (host array), in the unified model's output order:
+ *   [0] classificators_1 (n,512,1)  [1] classificators_2 (n,384,1)
+ *   [2] regressors_1 (n,512,16)     [3] regressors_2 (n,384,16)
+ *   [4] re_lu_10 tap (n,16,16,88)   [5] re_lu_15 tap (n,8,8,96)
+ * The two pose regressors of the unified model (`model` on re_lu_10, `model_10` on re_lu_15) run
+ * on the taps through hpe_forward (programs compiled with P = 256 and P = 64).
+ * workspace: hpe_blazeface_workspace_size(h, n_images) bytes of device memory. */
+typedef struct hpe_blazeface hpe_blazeface;
+int hpe_blazeface_create(const int32_t *words, int64_t n_words, hpe_blazeface **out);
+int hpe_blazeface_destroy(hpe_blazeface *h);
+size_t hpe_blazeface_workspace_size(const hpe_blazeface *h, int64_t n_images);
+int hpe_blazeface_forward(const hpe_blazeface *h, const float *params, const float *images,
+                          int64_t n_images, float *const *outs, void *workspace, void *stream);
+
 const char *hpe_last_error(void);
 
 #ifdef __cplusplus
