@@ -96,6 +96,71 @@ def cpu_baseline(weights_cfg, steps_budget_s=12.0):
             'cpu': _cpu_name()}
 
 
+BLAZE_B = 1024
+BLAZE_ID = 'reg1-stoqa9pt-reg2-hrchr82r-selected'
+
+
+def bench_blazeface(dev, iters, no_cpu):
+    """Config 5: the unified BlazeFace + stoqa9pt + hrchr82r graph (reference weights), batch 1024
+    frames of 128x128x3 uniform(-1, 1), fp32.  Roofline: the fused ops are each HBM-bound by
+    design (depthwise 1.9 FLOP/B), so achieved = the plan's algorithmic bytes (every op's input +
+    output map, hpe.blazeface.work_per_image) / the measured time of the whole forward."""
+    from hpe import blazeface as BF
+    gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
+    with open(os.path.join(gdir, BLAZE_ID + '.json')) as fh:
+        mc = json.load(fh)['model_config']
+    wts = dict(np.load(os.path.join(gdir, BLAZE_ID + '.npz')))
+    bf = BF.BlazeFace(mc, wts, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    x = (torch.rand((BLAZE_B, 128, 128, 3), generator=g, device=dev) * 2 - 1).contiguous()
+    for _ in range(3):
+        bf.forward(x)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(iters):
+        bf.forward(x)
+    e1.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / iters
+    ms = e0.elapsed_time(e1) / iters
+    flop, nbytes = BF.work_per_image(bf.plan)
+    res = {'workload': 'unified BlazeFace (16 dw/pw blocks, 4 detector heads) + stoqa9pt + hrchr82r '
+                       'pose heads, reference weights, batch %d frames 128x128x3 (configs[4])' % BLAZE_B,
+           'value': BLAZE_B / wall, 'unit': 'images/sec', 'ms_per_batch': wall * 1e3, 'dtype': 'fp32',
+           'data': 'synthetic uniform(-1,1) frames',
+           'roofline': {'bound': 'hbm', 'achieved': nbytes * BLAZE_B / (ms * 1e-3) / 1e9,
+                        'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
+                        'frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
+                        'traffic': _traffic('blazeface'),
+                        'kernel': 'bf_stem_kernel + 16 bf_block_kernel + 2 head GEMMs + 2 regressor '
+                                  'programs (hpe_blazeface_forward + hpe_forward)',
+                        'kernel_ms': ms, 'bytes_per_launch': nbytes * BLAZE_B,
+                        'flop_per_launch': flop * BLAZE_B,
+                        'mfma_frac': flop * BLAZE_B / (ms * 1e-3) / PEAK_FP32}}
+    if not no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import keras_ref as K
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        gr = K.Graph(mc, wts, dtype=torch.float32)
+        xs = np.random.default_rng(0).uniform(-1, 1, (8, 128, 128, 3)).astype(np.float32)
+        gr.forward(xs)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 10.0 or k < 2:
+            gr.forward(xs)
+            k += 1
+        dt = time.perf_counter() - t0
+        res['cpu_baseline'] = {'value': k * 8 / dt, 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+                               'sample': '%d forwards x 8 frames (oracle/keras_ref.py torch-CPU fp32), %.1f s'
+                                         % (k, dt)}
+    return res
+
+
 def _cpu_name():
     try:
         with open('/proc/cpuinfo') as fh:
@@ -125,6 +190,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-infer', action='store_true')
+    ap.add_argument('--no-blaze', action='store_true')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -252,6 +318,9 @@ def main():
                              ie.program('fwd', P).prog.kind, '?') + ' (hpe_forward)',
                          'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
                          'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
+    # ---- BlazeFace + both pose heads ----------------------------------
+    if rank == 0 and not a.no_blaze:
+        out['blazeface'] = bench_blazeface(dev, max(10, a.steps), a.no_cpu or world > 1)
     if rank == 0 and world == 1 and not a.no_cpu:
         cb = cpu_baseline((m.model_config, init_w))
         out['cpu_baseline'] = cb

@@ -454,3 +454,37 @@ class BlazeFace:
         x = torch.as_tensor(np.ascontiguousarray(images, np.float32)).to(self.device)
         outs = self.forward(x)
         return [o.cpu().numpy() for o in outs]
+
+
+def work_per_image(plan):
+    """Algorithmic work of one 128x128 frame through the plan: FLOP = 2*MAC of the
+    convs (depthwise, pointwise, stem, heads) and the regressors; bytes = each fused op's compulsory
+    HBM traffic (its input map + its output map, fp32, padded channel strides as stored) plus the
+    regressors' tap reads and pose writes."""
+    words = plan['words']
+    flop = 0
+    nbytes = 0
+    off = int(words[BFH_OPS_OFF])
+    for i in range(int(words[BFH_NOPS])):
+        f = [int(v) for v in words[off + i * BFO_WORDS: off + (i + 1) * BFO_WORDS]]
+        hw_in, hw_out = f[BFO_H] * f[BFO_W], f[BFO_HO] * f[BFO_WO]
+        if f[BFO_KIND] == BF_STEM:
+            flop += 2 * hw_out * 25 * 3 * f[BFO_COUT]
+            nbytes += 4 * (hw_in * 3 + hw_out * f[BFO_COUTP])
+            continue
+        if f[BFO_DW]:
+            flop += 2 * hw_out * 9 * f[BFO_CIN]
+        flop += 2 * hw_out * f[BFO_CIN] * f[BFO_COUT]
+        out_c = f[BFO_COUT] if f[BFO_SPLIT] else f[BFO_OSTRIDE]
+        nbytes += 4 * (hw_in * f[BFO_CINP] + hw_out * out_c)
+    st = plan['structure']
+    for r in st['regressors']:
+        h, w, c = st['shapes'][r['tap']]
+        layers = [l for l in r['config']['layers'] if l['class_name'] in ('Conv2D', 'Dense')]
+        cin = c
+        for l in layers:
+            n = l['config'].get('filters', l['config'].get('units'))
+            flop += 2 * h * w * cin * n
+            cin = n
+        nbytes += 4 * h * w * (c + 3)
+    return flop, nbytes
