@@ -26,6 +26,8 @@ SIGNATURES = {
     'hpe_blazeface_destroy': (ctypes.c_int, [_vp]),
     'hpe_blazeface_workspace_size': (_sz, [_vp, _i64]),
     'hpe_blazeface_forward': (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    'hpe_detect': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _i32, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp]),
     'hpe_last_error': (ctypes.c_char_p, []),
 }
 

@@ -114,6 +114,22 @@ size_t hpe_blazeface_workspace_size(const hpe_blazeface *h, int64_t n_images);
 int hpe_blazeface_forward(const hpe_blazeface *h, const float *params, const float *images,
                           int64_t n_images, float *const *outs, void *workspace, void *stream);
 
+/* Detector post-processing of the unified graph for a batch of frames,
+ * replacing blazeFaceDetector.filterDetections / extractDetections / filterWithNonMaxSupression
+ * (BlazePoser/blazeFaceDetectorH5.py:284-357) per frame:
+ *   keep logit > score_logit_threshold (fp32; the reference's log(t/(1-t))), score = sigmoid (fp32),
+ *   decode boxes / 6 keypoints against the 896 SSD anchors in fp64, greedy NMS with
+ *   tf.image.non_max_suppression semantics (IoU in fp32, suppress iff IoU > iou_threshold, at most
+ *   max_faces kept), and gather each kept detection's pose from its 16x16 / 8x8 regressor cell.
+ * Inputs (device): cls0 (n,512), cls1 (n,384), loc0 (n,512,16), loc1 (n,384,16), pose0 (n,16,16,3),
+ * pose1 (n,8,8,3).  Outputs (device, per frame max_faces slots, the first count[i] valid, in NMS
+ * selection order): det_index int32, scores f32, boxes f64 [x1,y1,x2,y2], keypoints f64 [6][2],
+ * poses f32 [yaw, pitch, roll]. */
+int hpe_detect(const float *cls0, const float *cls1, const float *loc0, const float *loc1,
+               const float *pose0, const float *pose1, int64_t n_images, float score_logit_threshold,
+               float iou_threshold, int32_t max_faces, int32_t *count, int32_t *det_index, float *scores,
+               double *boxes, double *keypoints, float *poses, void *stream);
+
 const char *hpe_last_error(void);
 
 #ifdef __cplusplus

@@ -142,8 +142,7 @@ class Graph:
         mc = model_config.get('config', model_config)
         self.name = mc.get('name', 'model')
         self.dtype = dtype
-        self.layers = {l['config']['name'] if 'name' in l['config'] else l['name']: l
-                       for l in mc['layers']}
+        self.layers = {l.get('name', l['config'].get('name')): l for l in mc['layers']}
         self.order = [l['name'] for l in mc['layers']]
         self.inputs = [t[0] for t in mc['input_layers']]
         self.outputs = [t[0] for t in mc['output_layers']]
