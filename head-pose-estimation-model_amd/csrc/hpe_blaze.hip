@@ -54,26 +54,29 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
   const int H = f[BFO_H], W = f[BFO_W], Wo = f[BFO_WO], Ho = f[BFO_HO];
   const int TH = f[BFO_TH], ROWS = f[BFO_ROWS], COLS = f[BFO_COLS];
   const int Cout = f[BFO_COUT];
+  const int lgWo = __builtin_ctz(Wo);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
   const int tpi = Ho / TH;
   const int wid = xcd_work_id(a.nwg);
   const int64_t img = wid / tpi;
-  const int oy0 = (wid % tpi) * TH;
+  const int oy0 = (wid - (int)img * tpi) * TH;
   const float* P_ = a.params;
   // weights: W^T padded [32][90] (k = (ky*5 + kx)*3 + c, ky < 6), lane n = l32, its half's 45 k
   float wr[STEM_KS];
 #pragma unroll
   for (int s = 0; s < STEM_KS; ++s) wr[s] = P_[f[BFO_PWW] + l32 * 90 + half * STEM_KS + s];
-  // image tile rows iy = 2*oy0 - 1 + r, cols ix = c - 1, channel stride 3
+  // image tile: LDS row r <-> image row 2*oy0 - padt + r; a row is W*3 contiguous floats placed at
+  // column padl (zeros around), no per-element division
   const int iy0 = oy0 * 2 - f[BFO_PADT];
-  const int nflt = ROWS * COLS * 3;
-  for (int e = threadIdx.x; e < nflt; e += blockDim.x) {
-    const int r = e / (COLS * 3), rem = e - r * COLS * 3;
-    const int c = rem / 3, ch = rem - c * 3;
-    const int iy = iy0 + r, ix = c - f[BFO_PADL];
-    float v = 0.f;
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W && img < a.nimg) v = a.src[((img * H + iy) * W + ix) * 3 + ch];
-    lds[e] = v;
+  const int padl3 = f[BFO_PADL] * 3, rowf = COLS * 3, W3 = W * 3;
+  for (int r = 0; r < ROWS; ++r) {
+    const int iy = iy0 + r;
+    const bool rin = iy >= 0 && iy < H && img < a.nimg;
+    const float* srow = a.src + ((img * H + (rin ? iy : 0)) * W) * 3;
+    for (int e = threadIdx.x; e < rowf; e += blockDim.x) {
+      const int x3 = e - padl3;
+      lds[r * rowf + e] = (rin && x3 >= 0 && x3 < W3) ? srow[x3] : 0.f;
+    }
   }
   __syncthreads();
   if (img >= a.nimg) return;
@@ -81,21 +84,21 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
   const float bias = l32 < Cout ? P_[f[BFO_PWB] + l32] : 0.f;
   for (int chunk = wave; chunk * 32 < npos; chunk += blockDim.x >> 6) {
     const int p = chunk * 32 + l32;
-    const int oyl = p / Wo, ox = p - oyl * Wo;
-    const float* t = lds + ((oyl * 2 + half * 3) * COLS + ox * 2) * 3;
+    const int oyl = p >> lgWo, ox = p & (Wo - 1);
+    const float* t = lds + (oyl * 2 + half * 3) * rowf + ox * 6;
     f32x16 acc = {};
 #pragma unroll
     for (int s = 0; s < STEM_KS; ++s) {
       const int kyl = s / 15, kx = (s / 3) % 5, c = s % 3;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(t[(kyl * COLS + kx) * 3 + c], wr[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(t[kyl * rowf + kx * 3 + c], wr[s], acc, 0, 0, 0);
     }
     if (l32 < Cout) {
+      float* drow = a.dst + ((img * Ho + oy0) * Wo) * Cout + l32;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        const int qy = q / Wo, qx = q - qy * Wo;
+        const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;   // q = qy * Wo + qx
         const float v = acc[g] + bias;
-        a.dst[((img * Ho + oy0 + qy) * Wo + qx) * Cout + l32] = v > 0.f ? v : 0.f;
+        drow[q * Cout] = v > 0.f ? v : 0.f;
       }
     }
   }
@@ -103,10 +106,13 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // block: [depthwise 3x3 (S, TF 'same') ->] 1x1 conv (MFMA) -> + residual -> [ReLU]
-// LDS: W^T [NC*32][KS] | depthwise taps [9][Cinp] + bias [Cinp] | tile [NI][ROWS][COLS][CS]
+// LDS: W^T [NCT*32][KS] | depthwise taps [9][Cinp] + bias [Cinp] | tile [NI][ROWS][COLS][CS]
+// A wave task is (32-position chunk, group of NC output-channel chunks of 32): the depthwise A
+// operand is recomputed per group (cheap VALU next to the MFMA) to give every WG >= 4 waves.
+// Wo and TH*Wo are powers of two (checked on the host), so position math is shifts.
 // ------------------------------------------------------------------------------------------------
 template <int S, int DW, int NC>
-__global__ void __launch_bounds__(256) bf_block_kernel(BfArgs a) {
+__global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* f = a.f;
   const int H = f[BFO_H], W = f[BFO_W], Ho = f[BFO_HO], Wo = f[BFO_WO];
@@ -114,60 +120,74 @@ __global__ void __launch_bounds__(256) bf_block_kernel(BfArgs a) {
   const int TH = f[BFO_TH], NI = f[BFO_NI], ROWS = f[BFO_ROWS], COLS = f[BFO_COLS];
   const int CS = f[BFO_CS], KS = f[BFO_KS], padt = f[BFO_PADT], padl = f[BFO_PADL];
   const int res = f[BFO_RES], relu = f[BFO_RELU], split = f[BFO_SPLIT], ostride = f[BFO_OSTRIDE];
+  const int NCT = f[BFO_NCT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int lgWo = __builtin_ctz(Wo), lgP = __builtin_ctz(TH * Wo);
   const float* P_ = a.params;
   float* wt = lds;
-  float* dwt = wt + NC * 32 * KS;
+  float* dwt = wt + NCT * 32 * KS;
   float* tile = dwt + (DW ? 10 * Cinp : 0);
 
   const int tpi = Ho / TH;
   const int wid = xcd_work_id(a.nwg);
   const int64_t img0 = NI > 1 ? (int64_t)wid * NI : wid / tpi;
-  const int oy0 = NI > 1 ? 0 : (wid % tpi) * TH;
+  const int oy0 = NI > 1 ? 0 : (wid - (int)img0 * tpi) * TH;
 
   // ---- stage W^T (rows >= Coutp zero), depthwise table, input tile (zero outside the image) ----
+  // thread -> (quad q, first column c0), column step cstep: one division per thread, none in loops
   const int kq = Cinp >> 2;
-  for (int i = threadIdx.x; i < NC * 32 * kq; i += blockDim.x) {
-    const int n = i / kq, q = i - n * kq;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (n < Coutp) v = ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * q);
-    *(f32x4*)(wt + n * KS + 4 * q) = v;
+  const int nthr = blockDim.x;
+  const int tq = threadIdx.x % kq, tc = threadIdx.x / kq, cstep = nthr / kq;
+  if (tc < cstep) {
+    for (int n = tc; n < NCT * 32; n += cstep) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (n < Coutp) v = ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * tq);
+      *(f32x4*)(wt + n * KS + 4 * tq) = v;
+    }
+    const int iy0 = oy0 * S - padt;
+    for (int il = 0; il < NI; ++il) {
+      const int64_t img = img0 + il;
+      for (int r = 0; r < ROWS; ++r) {
+        const int iy = iy0 + r;
+        const bool rin = iy >= 0 && iy < H && img < a.nimg;
+        const float* srow = a.src + ((img * H + (rin ? iy : 0)) * W) * Cinp + 4 * tq;
+        float* lrow = tile + ((il * ROWS + r) * COLS) * CS + 4 * tq;
+        for (int c = tc; c < COLS; c += cstep) {
+          const int ix = c - padl;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (rin && ix >= 0 && ix < W) v = ld4(srow + ix * Cinp);
+          *(f32x4*)(lrow + c * CS) = v;
+        }
+      }
+    }
   }
   if (DW)
-    for (int i = threadIdx.x; i < 10 * kq; i += blockDim.x) *(f32x4*)(dwt + 4 * i) = ld4(P_ + f[BFO_DWW] + 4 * i);
-  const int iy0 = oy0 * S - padt;
-  const int per_img = ROWS * COLS * kq;
-  for (int i = threadIdx.x; i < NI * per_img; i += blockDim.x) {
-    const int il = i / per_img, rem = i - il * per_img;
-    const int r = rem / (COLS * kq), rem2 = rem - r * COLS * kq;
-    const int c = rem2 / kq, q = rem2 - c * kq;
-    const int iy = iy0 + r, ix = c - padl;
-    const int64_t img = img0 + il;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W && img < a.nimg)
-      v = ld4(a.src + ((img * H + iy) * W + ix) * Cinp + 4 * q);
-    *(f32x4*)(tile + ((il * ROWS + r) * COLS + c) * CS + 4 * q) = v;
-  }
+    for (int i = threadIdx.x; i < 10 * kq; i += nthr) *(f32x4*)(dwt + 4 * i) = ld4(P_ + f[BFO_DWW] + 4 * i);
   __syncthreads();
 
-  const int ppi = TH * Wo;  // output positions per image in this tile
-  const int npos = NI * ppi;
-  const int nwaves = blockDim.x >> 6;
-  for (int chunk = wave; chunk * 32 < npos; chunk += nwaves) {
+  const int npos = NI * TH * Wo;
+  const int ngrp = NCT / NC;
+  const int ntask = (npos >> 5) * ngrp;
+  const int nwaves = nthr >> 6;
+  const int colsCS = COLS * CS;
+  for (int task = wave; task < ntask; task += nwaves) {
+    const int chunk = task / ngrp, grp = task - chunk * ngrp;
     const int p = chunk * 32 + l32;
-    const int il = p / ppi, pr = p - il * ppi;
-    const int oyl = pr / Wo, ox = pr - oyl * Wo;
-    const float* tb = tile + ((il * ROWS + oyl * S) * COLS + ox * S) * CS;
+    const int il = p >> lgP, pr = p & ((1 << lgP) - 1);
+    const int oyl = pr >> lgWo, ox = pr & (Wo - 1);
+    const float* tb = tile + (il * ROWS + oyl * S) * colsCS + ox * S * CS;
+    const float* wb = wt + (grp * NC * 32 + l32) * KS;
     f32x16 acc[NC];
 #pragma unroll
     for (int nc = 0; nc < NC; ++nc) acc[nc] = (f32x16){};
+#pragma unroll 2
     for (int c0 = 4 * half; c0 < Cinp; c0 += 8) {
       f32x4 av;
       if (DW) {
         av = ld4(dwt + 9 * Cinp + c0);
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
-          const f32x4 xv = ld4(tb + ((tp / 3) * COLS + (tp % 3)) * CS + c0);
+          const f32x4 xv = ld4(tb + (tp / 3) * colsCS + (tp % 3) * CS + c0);
           const f32x4 wv = ld4(dwt + tp * Cinp + c0);
           av.x = fmaf(xv.x, wv.x, av.x);
           av.y = fmaf(xv.y, wv.y, av.y);
@@ -179,7 +199,7 @@ __global__ void __launch_bounds__(256) bf_block_kernel(BfArgs a) {
       }
 #pragma unroll
       for (int nc = 0; nc < NC; ++nc) {
-        const f32x4 bv = ld4(wt + (nc * 32 + l32) * KS + c0);
+        const f32x4 bv = ld4(wb + nc * 32 * KS + c0);
         acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[nc], 0, 0, 0);
         acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[nc], 0, 0, 0);
         acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc[nc], 0, 0, 0);
@@ -189,21 +209,21 @@ __global__ void __launch_bounds__(256) bf_block_kernel(BfArgs a) {
     // ---- epilogue: lane = output channel n, registers = 16 positions of the chunk ----
 #pragma unroll
     for (int nc = 0; nc < NC; ++nc) {
-      const int n = nc * 32 + l32;
+      const int n = (grp * NC + nc) * 32 + l32;
       if (n >= Coutp) continue;
       const float bias = P_[f[BFO_PWB] + n];
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        const int ql = q / ppi, qr = q - ql * ppi;
-        const int qy = qr / Wo, qx = qr - qy * Wo;
+        const int ql = q >> lgP, qr = q & ((1 << lgP) - 1);
+        const int qy = qr >> lgWo, qx = qr & (Wo - 1);
         float v = acc[nc][g] + bias;
         if (res == BF_RES_ID) {
-          if (n < Cinp) v += tile[((ql * ROWS + qy + padt) * COLS + qx + padl) * CS + n];
+          if (n < Cinp) v += tile[(ql * ROWS + qy + padt) * colsCS + (qx + padl) * CS + n];
         } else if (res == BF_RES_MAXPOOL) {
           if (n < Cinp) {
-            const float* t = tile + ((ql * ROWS + 2 * qy) * COLS + 2 * qx) * CS + n;
-            v += fmaxf(fmaxf(t[0], t[CS]), fmaxf(t[COLS * CS], t[(COLS + 1) * CS]));
+            const float* t = tile + (ql * ROWS + 2 * qy) * colsCS + 2 * qx * CS + n;
+            v += fmaxf(fmaxf(t[0], t[CS]), fmaxf(t[colsCS], t[colsCS + CS]));
           }
         }
         if (relu) v = v > 0.f ? v : 0.f;
@@ -258,6 +278,9 @@ static int check_op(const int* f, int i) {
   if (f[BFO_LDS] <= 0 || f[BFO_LDS] > 160 * 1024) return hpe_fail(HPE_EINVAL, "blazeface op %d: LDS %d bytes", i, f[BFO_LDS]);
   if (f[BFO_SRC] < 0 || f[BFO_SRC] >= BF_NBUF || f[BFO_DST] < 0 || f[BFO_DST] >= BF_NBUF)
     return hpe_fail(HPE_EINVAL, "blazeface op %d: bad buffer", i);
+  const int wo = f[BFO_WO], ppi = f[BFO_TH] * f[BFO_WO];
+  if (wo <= 0 || (wo & (wo - 1)) || (ppi & (ppi - 1))) return hpe_fail(HPE_EINVAL, "blazeface op %d: Wo and TH*Wo must be powers of two", i);
+  if (f[BFO_WAVES] < 1 || f[BFO_WAVES] > (kind == BF_STEM ? 4 : 8)) return hpe_fail(HPE_EINVAL, "blazeface op %d: waves", i);
   if (kind == BF_STEM) {
     if (f[BFO_CIN] != 3 || f[BFO_COUT] > 32 || f[BFO_STRIDE] != 2) return hpe_fail(HPE_EINVAL, "blazeface stem: unsupported geometry");
     const int rows = 2 * (f[BFO_TH] - 1) + 6, cols = 2 * (f[BFO_WO] - 1) + 5;
@@ -266,9 +289,11 @@ static int check_op(const int* f, int i) {
     return 0;
   }
   const int s = f[BFO_STRIDE], dw = f[BFO_DW];
+  if (f[BFO_NCT] < 1 || f[BFO_NCT] * 32 < f[BFO_COUTP] || f[BFO_NCT] % f[BFO_NC] || f[BFO_CINP] / 4 > 64 * f[BFO_WAVES])
+    return hpe_fail(HPE_EINVAL, "blazeface op %d: channel chunks", i);
   if (!pick_block(s, dw, f[BFO_NC])) return hpe_fail(HPE_EINVAL, "blazeface op %d: no kernel for S=%d DW=%d NC=%d", i, s, dw, f[BFO_NC]);
   if (f[BFO_CINP] % 8 || f[BFO_CINP] < f[BFO_CIN] || f[BFO_COUTP] % 8 || f[BFO_COUTP] < f[BFO_COUT] ||
-      f[BFO_NC] * 32 < f[BFO_COUTP] || f[BFO_CS] < f[BFO_CINP] || f[BFO_CS] % 4 || f[BFO_KS] < f[BFO_CINP] || f[BFO_KS] % 4)
+      f[BFO_CS] < f[BFO_CINP] || f[BFO_CS] % 4 || f[BFO_KS] < f[BFO_CINP] || f[BFO_KS] % 4)
     return hpe_fail(HPE_EINVAL, "blazeface op %d: channel geometry", i);
   const int rows = dw ? (f[BFO_TH] - 1) * s + 3 : f[BFO_TH];
   const int cols = dw ? (f[BFO_WO] - 1) * s + 3 : f[BFO_WO];
@@ -276,7 +301,7 @@ static int check_op(const int* f, int i) {
   if (f[BFO_RES] == BF_RES_MAXPOOL && (s != 2 || f[BFO_H] % 2 || f[BFO_W] % 2 || f[BFO_PADT] || f[BFO_PADL]))
     return hpe_fail(HPE_EINVAL, "blazeface op %d: maxpool residual needs s2 on even maps", i);
   if (f[BFO_RES] == BF_RES_ID && s != 1) return hpe_fail(HPE_EINVAL, "blazeface op %d: identity residual needs s1", i);
-  const long need = 4L * (f[BFO_NC] * 32 * f[BFO_KS] + (dw ? 10 * f[BFO_CINP] : 0) +
+  const long need = 4L * (f[BFO_NCT] * 32 * f[BFO_KS] + (dw ? 10 * f[BFO_CINP] : 0) +
                           (long)f[BFO_NI] * rows * cols * f[BFO_CS]);
   if (f[BFO_LDS] < need) return hpe_fail(HPE_EINVAL, "blazeface op %d: LDS words %d < %ld", i, f[BFO_LDS], need);
   if (!f[BFO_SPLIT] && (f[BFO_OSTRIDE] < f[BFO_COUT] || f[BFO_OSTRIDE] > f[BFO_COUTP]))
@@ -345,9 +370,7 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
     const int64_t nwg = f[BFO_NI] > 1 ? (n_images + f[BFO_NI] - 1) / f[BFO_NI] : n_images * tpi;
     if (nwg > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
     a.nwg = (int)nwg;
-    const int npos = f[BFO_NI] * f[BFO_TH] * f[BFO_WO];
-    const int chunks = npos / 32;
-    const int threads = 64 * (chunks < 4 ? chunks : 4);
+    const int threads = 64 * f[BFO_WAVES];
     bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(threads), f[BFO_LDS], s, a);

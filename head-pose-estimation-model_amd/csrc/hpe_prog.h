@@ -81,5 +81,5 @@ enum {
   BFO_KIND = 0, BFO_H, BFO_W, BFO_HO, BFO_WO, BFO_CIN, BFO_COUT, BFO_CINP, BFO_COUTP,
   BFO_STRIDE, BFO_PADT, BFO_PADL, BFO_DW, BFO_RES, BFO_RELU, BFO_SRC, BFO_DST, BFO_DST2,
   BFO_SPLIT, BFO_TH, BFO_NI, BFO_DWW, BFO_PWW, BFO_PWB, BFO_CS, BFO_KS, BFO_ROWS, BFO_COLS,
-  BFO_NC, BFO_LDS, BFO_OSTRIDE, BFO_WORDS = 32
+  BFO_NC, BFO_LDS, BFO_OSTRIDE, BFO_NCT, BFO_WAVES, BFO_WORDS = 40
 };

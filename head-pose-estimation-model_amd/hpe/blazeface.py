@@ -30,9 +30,8 @@ BUF_IMG, BUF_A, BUF_B, BUF_OUT0 = 0, 1, 2, 3
 (BFO_KIND, BFO_H, BFO_W, BFO_HO, BFO_WO, BFO_CIN, BFO_COUT, BFO_CINP, BFO_COUTP,
  BFO_STRIDE, BFO_PADT, BFO_PADL, BFO_DW, BFO_RES, BFO_RELU, BFO_SRC, BFO_DST, BFO_DST2,
  BFO_SPLIT, BFO_TH, BFO_NI, BFO_DWW, BFO_PWW, BFO_PWB, BFO_CS, BFO_KS, BFO_ROWS, BFO_COLS,
- BFO_NC, BFO_LDS, BFO_OSTRIDE) = range(31)
-BFO_WORDS = 32
-LDS_BUDGET = 64 * 1024      # keep >= 2 workgroups per CU
+ BFO_NC, BFO_LDS, BFO_OSTRIDE, BFO_NCT, BFO_WAVES) = range(33)
+BFO_WORDS = 40
 STEM_TH = 4
 
 
@@ -166,7 +165,11 @@ def parse(model_config):
             if cls(conv) != 'Conv2D' or tuple(cc['kernel_size']) != (1, 1) or cc['activation'] != 'linear' \
                     or tap not in shapes or tap == stem:
                 raise ValueError('output %s: expected Reshape(linear 1x1 conv(block output))' % o)
-            heads.append(dict(out=o, conv=conv, tap=tap, n=cc['filters']))
+            tshape = [int(v) for v in conf(o)['constants']['1']][1:]
+            th_, tw_, _ = shapes[tap]
+            if int(np.prod(tshape)) != th_ * tw_ * cc['filters']:
+                raise ValueError('output %s: Reshape %s does not match %s' % (o, tshape, (th_, tw_, cc['filters'])))
+            heads.append(dict(out=o, conv=conv, tap=tap, n=cc['filters'], shape=tuple(tshape)))
         elif oc == 'Functional':
             rs = only(ins[o], 'regressor input')
             tap = rs
@@ -206,26 +209,35 @@ class _Params:
         return np.concatenate(self.chunks) if self.chunks else np.zeros(0, np.float32)
 
 
-def _block_tile(ho, wo, s, dw, cinp, nc, ks, cs):
-    """Largest tile (TH rows of one image, or NI whole images) with 128..256 positions within the
-    LDS budget; falls back to the smallest legal one."""
+def _block_tile(ho, wo, s, dw, cinp, nct, ks, cs):
+    """Pick the tile (TH rows of one image, or NI whole images), the output-channel chunks per wave
+    task (NC) and the waves per workgroup: maximise resident waves per CU (LDS-limited, capped at
+    16), then minimise the halo re-read factor, then prefer more channel chunks per task (no
+    depthwise recompute).  Wo and TH*Wo must be powers of two (kernel uses shifts)."""
     best = None
-    cands = []
-    for th in [d for d in range(1, ho + 1) if ho % d == 0]:
-        cands.append((th, 1))
-    for ni in (2, 4, 8):
-        cands.append((ho, ni))
+    cands = [(th, 1) for th in range(1, ho + 1) if ho % th == 0] + [(ho, ni) for ni in (2, 4, 8)]
     for th, ni in cands:
         npos = ni * th * wo
-        if npos % 32 or npos > 256:
+        ppi = th * wo
+        if npos % 32 or npos > 512 or (ppi & (ppi - 1)) or (wo & (wo - 1)):
             continue
         rows = (th - 1) * s + 3 if dw else th
         cols = (wo - 1) * s + 3 if dw else wo
-        lds = 4 * (nc * 32 * ks + (10 * cinp if dw else 0) + ni * rows * cols * cs)
-        key = (lds <= LDS_BUDGET, npos if lds <= LDS_BUDGET else -lds)
-        if best is None or key > best[0]:
-            best = (key, th, ni, rows, cols, lds)
-    if best is None or best[5] > 160 * 1024:
+        lds = 4 * (nct * 32 * ks + (10 * cinp if dw else 0) + ni * rows * cols * cs)
+        if lds > 160 * 1024:
+            continue
+        for nc in [d for d in (1, 2, 3, 4) if nct % d == 0]:
+            tasks = (npos // 32) * (nct // nc)
+            waves = min(tasks, 8)
+            if cinp // 4 > 64 * waves:
+                continue
+            vg_waves = 8 if nc <= 2 else 5            # waves/SIMD the VGPR budget allows
+            per_cu = min((160 * 1024) // lds * waves, 4 * vg_waves, 16)
+            halo = rows * cols / float(th * wo * s * s)
+            key = (per_cu, -round(halo, 3), nc)
+            if best is None or key > best[0]:
+                best = (key, th, ni, rows, cols, lds, nc, waves)
+    if best is None:
         raise ValueError('no BlazeFace tile fits LDS for %dx%d Cin %d' % (ho, wo, cinp))
     return best[1:]
 
@@ -261,6 +273,7 @@ def build_plan(model_config, weights):
     f[BFO_SRC], f[BFO_DST] = BUF_IMG, BUF_A
     f[BFO_TH], f[BFO_NI], f[BFO_PWW], f[BFO_PWB] = STEM_TH, 1, pww, pwb
     f[BFO_ROWS], f[BFO_COLS], f[BFO_NC], f[BFO_LDS] = rows, cols, 1, rows * cols * 12
+    f[BFO_NCT], f[BFO_WAVES] = 1, min(4, STEM_TH * wo // 32)
     if _r8(cout) != cout:
         raise ValueError('stem filters %d: multiple of 8 required' % cout)
     ops.append(f)
@@ -286,10 +299,10 @@ def build_plan(model_config, weights):
         bb = np.zeros(coutp, np.float32)
         bb[:cout] = wk(bl['pw'], 'bias')
         pwb = P.add(bb)
-        nc = -(-coutp // 32)
+        nct = -(-coutp // 32)
         s = bl['stride']
         cs = ks = cinp + 4                                    # (cs/4) odd: conflict-free b128 rows
-        th, ni, rows, cols, lds = _block_tile(bl['Ho'], bl['Wo'], s, True, cinp, nc, ks, cs)
+        th, ni, rows, cols, lds, nc, waves = _block_tile(bl['Ho'], bl['Wo'], s, True, cinp, nct, ks, cs)
         if bl['out'] in tap_buf:
             dst = tap_buf[bl['out']]
             if coutp != cout:
@@ -305,7 +318,7 @@ def build_plan(model_config, weights):
         f[BFO_SRC], f[BFO_DST] = cur_buf, dst
         f[BFO_TH], f[BFO_NI], f[BFO_DWW], f[BFO_PWW], f[BFO_PWB] = th, ni, dww, pww, pwb
         f[BFO_CS], f[BFO_KS], f[BFO_ROWS], f[BFO_COLS], f[BFO_NC], f[BFO_LDS] = cs, ks, rows, cols, nc, lds
-        f[BFO_OSTRIDE] = coutp
+        f[BFO_OSTRIDE], f[BFO_NCT], f[BFO_WAVES] = coutp, nct, waves
         ops.append(f)
         if dst in (BUF_A, BUF_B):
             act_floats = max(act_floats, bl['Ho'] * bl['Wo'] * coutp)
@@ -334,11 +347,11 @@ def build_plan(model_config, weights):
             bb[o:o + h['n']] = wk(h['conv'], 'bias')
             o += h['n']
         pww, pwb = P.add(wt), P.add(bb)
-        nc = -(-coutp // 32)
-        if nc > 4:
+        nct = -(-coutp // 32)
+        if nct > 4:
             raise ValueError('detector heads on %s: %d channels > 128' % (tap, cout))
         cs = ks = cinp + 4
-        th, ni, rows, cols, lds = _block_tile(th_, tw_, 1, False, cinp, nc, ks, cs)
+        th, ni, rows, cols, lds, nc, waves = _block_tile(th_, tw_, 1, False, cinp, nct, ks, cs)
         f = [0] * BFO_WORDS
         f[BFO_KIND], f[BFO_H], f[BFO_W], f[BFO_HO], f[BFO_WO] = BF_BLOCK, th_, tw_, th_, tw_
         f[BFO_CIN], f[BFO_COUT], f[BFO_CINP], f[BFO_COUTP] = cin, cout, cinp, coutp
@@ -350,6 +363,7 @@ def build_plan(model_config, weights):
             f[BFO_SPLIT], f[BFO_DST2], f[BFO_OSTRIDE] = 0, -1, cout
         f[BFO_TH], f[BFO_NI], f[BFO_PWW], f[BFO_PWB] = th, ni, pww, pwb
         f[BFO_CS], f[BFO_KS], f[BFO_ROWS], f[BFO_COLS], f[BFO_NC], f[BFO_LDS] = cs, ks, rows, cols, nc, lds
+        f[BFO_NCT], f[BFO_WAVES] = nct, waves
         ops.append(f)
     hdr = [0] * BFH_WORDS
     hdr[BFH_MAGIC], hdr[BFH_NOPS], hdr[BFH_ACT_FLOATS], hdr[BFH_OPS_OFF] = BF_MAGIC, len(ops), act_floats, BFH_WORDS
@@ -404,9 +418,8 @@ class BlazeFace:
     def output_shapes(self, n):
         st = self.structure
         shp = {}
-        for i, hd in enumerate(st['heads']):
-            th, tw, _ = st['shapes'][hd['tap']]
-            shp[hd['out']] = (n, th * tw, hd['n'])
+        for hd in st['heads']:
+            shp[hd['out']] = (n,) + hd['shape']
         for r, _ in self.regs:
             th, tw, _ = st['shapes'][r['tap']]
             shp[r['out']] = (n, th, tw, 3)

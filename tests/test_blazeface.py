@@ -39,7 +39,8 @@ def test_structure_recognised():
     assert st['taps'] == ['re_lu_10', 're_lu_15']
     assert st['shapes']['re_lu_10'] == (16, 16, 88) and st['shapes']['re_lu_15'] == (8, 8, 96)
     assert [r['out'] for r in st['regressors']] == ['model', 'model_10']
-    assert len(st['heads']) == 4
+    assert len(st["heads"]) == 4
+    assert [h["shape"] for h in st["heads"]] == [(512, 1), (384, 1), (512, 16), (384, 16)]
 
 
 def test_plan_words_emulated_match_oracle():
