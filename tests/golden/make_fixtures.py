@@ -34,6 +34,9 @@ NAMED = ['stoqa9pt', 'ker7z9mv', '9w31h50k', '4121t6zb', 'hrchr82r', 'model_runi
          'sqnu665j', 'o6e5xpan', '0g73t16n', 'cl4obelj']
 OPT_STATE = ['0g73t16n', 'stoqa9pt']
 MAX_BYTES = 400_000
+# the four fused BlazeFace + regressor graphs (BlazePoser/UnifiedModels, blazeFaceDetectorH5.py:97-101)
+UNIFIED = ['reg1-stoqa9pt-reg2-hrchr82r-selected', 'reg1-stoqa9pt-reg2-cl4obelj', 'reg1-9w31h50k-reg2-cl4obelj',
+           'reg1-4121t6zb-reg2-cl4obelj']
 DATASETS = ['AFLW2000_features_88_0.7_1.npz', 'AFLW2000_features_96_0.7_1.npz',
             'AFLW2000_Enlarged_features_88_0.7_1.npz', 'BIWI_train_features_88.npz',
             'BIWI_test_features_88.npz', 'BIWI_Test_Enlarged_features_88_0.7_1.npz',
@@ -114,8 +117,8 @@ def main():
         if rid in NAMED:
             chosen[rid] = p
     # the fused BlazeFace + both heads graph that blazeFaceDetectorH5.py:102 loads (config 5)
-    chosen['reg1-stoqa9pt-reg2-hrchr82r-selected'] = (
-        REF + '/BlazePoser/UnifiedModels/reg1-stoqa9pt-reg2-hrchr82r-selected.h5')
+    for u in UNIFIED:
+        chosen[u] = REF + '/BlazePoser/UnifiedModels/%s.h5' % u
     index = {}
     for rid, p in sorted(chosen.items()):
         key = rid

@@ -18,6 +18,7 @@ from oracle import keras_ref as K
 from util import fixture
 
 RID = 'reg1-stoqa9pt-reg2-hrchr82r-selected'
+UNIFIED = [RID, 'reg1-stoqa9pt-reg2-cl4obelj', 'reg1-9w31h50k-reg2-cl4obelj', 'reg1-4121t6zb-reg2-cl4obelj']
 BF_RTOL, BF_ATOL = 1e-4, 1e-3
 
 
@@ -43,8 +44,9 @@ def test_structure_recognised():
     assert [h["shape"] for h in st["heads"]] == [(512, 1), (384, 1), (512, 16), (384, 16)]
 
 
-def test_plan_words_emulated_match_oracle():
-    mc, w = fixture(RID)
+@pytest.mark.parametrize('rid', UNIFIED)
+def test_plan_words_emulated_match_oracle(rid):
+    mc, w = fixture(rid)
     plan = B.build_plan(mc, w)
     x = _images(2, seed=1)
     bufs = blaze_emu.run(plan, x)
@@ -95,9 +97,9 @@ def test_capi_validates_plan_without_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('n', [1, 5, 33])
-def test_blazeface_forward_matches_oracle(n):
-    mc, w = fixture(RID)
+@pytest.mark.parametrize('rid,n', [(RID, 1), (RID, 5), (RID, 33)] + [(u, 3) for u in UNIFIED[1:]])
+def test_blazeface_forward_matches_oracle(rid, n):
+    mc, w = fixture(rid)
     bf = B.BlazeFace(mc, w)
     x = _images(n, seed=n)
     got = bf.predict(x)
