@@ -501,3 +501,48 @@ def work_per_image(plan):
             cin = n
         nbytes += 4 * h * w * (c + 3)
     return flop, nbytes
+
+
+class UnifiedModel:
+    """Keras-model-shaped wrapper of a unified BlazeFace graph (what ``keras.models.load_model`` on
+    ``BlazePoser/UnifiedModels/*.h5`` returns in the reference, blazeFaceDetectorH5.py:101):
+    inference only — the reference never trains this graph."""
+
+    def __init__(self, model_config, weights, name=None):
+        self.model_config = model_config if 'config' in model_config else {'class_name': 'Functional',
+                                                                            'config': model_config}
+        self.name = name or self.model_config['config'].get('name', 'model')
+        self._weights = dict(weights)
+        self._bf = None
+        parse(self.model_config)          # structure errors surface at load time (ValueError)
+
+    def _net(self):
+        if self._bf is None:
+            self._bf = BlazeFace(self.model_config, self._weights)
+        return self._bf
+
+    def predict(self, x, batch_size=None, verbose=0, **kw):
+        return self._net().predict(x)
+
+    def __call__(self, x, training=False):
+        if torch.is_tensor(x) and x.is_cuda:
+            return self._net().forward(x)
+        return self.predict(x)
+
+    def count_params(self):
+        return int(sum(np.asarray(v).size for v in self._weights.values()))
+
+    def get_weights(self):
+        return [np.asarray(v) for v in self._weights.values()]
+
+    def weights_dict(self):
+        return dict(self._weights)
+
+    def to_json(self):
+        import json
+        return json.dumps(self.model_config)
+
+    def compile(self, *a, **k):
+        raise NotImplementedError('the unified BlazeFace graph is inference-only (as in the reference)')
+
+    fit = compile

@@ -326,6 +326,9 @@ class Model:
 
 def model_from_config(model_config, weights, name=None):
     cfg = model_config.get('config', model_config)
+    from . import blazeface
+    if blazeface.is_blazeface(cfg):
+        return blazeface.UnifiedModel({'class_name': 'Functional', 'config': cfg}, weights, name=name)
     return Model(name=name or cfg.get('name'), _config=cfg, _weights=weights)
 
 

@@ -121,3 +121,13 @@ def test_blazeface_taps_match_oracle():
         cfg['output_layers'] = [[t, 0, 0]]
         ref = K.Graph(dict(mc, config=cfg), w).forward(x).detach().numpy()
         np.testing.assert_allclose(dev.cpu().numpy(), ref, rtol=BF_RTOL, atol=BF_ATOL, err_msg=t)
+
+
+def test_load_model_returns_unified_wrapper():
+    import hpe
+    from util import MODELS
+    u = hpe.load_model(MODELS + '/' + RID)
+    assert type(u).__name__ == 'UnifiedModel'
+    assert u.count_params() == 101390 + 5891 + 3683       # backbone + stoqa9pt + hrchr82r
+    with pytest.raises(NotImplementedError):
+        u.compile(optimizer='adam')
