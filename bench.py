@@ -96,6 +96,58 @@ def cpu_baseline(weights_cfg, steps_budget_s=12.0):
             'cpu': _cpu_name()}
 
 
+def bench_train88(hpe, keras, dev, steps, warmup):
+    """Model-88 training on synthetic 88x88 maps (north_star's 88x88 line; configs[2] topology): the
+    train_88.py create_model graph (88 -> 64 softsign -> SpatialDropout(1e-4) -> 3 -> SpatialDropout,
+    L2 1e-6 on kernels, train_88.py:66-140), legacy Adam lr 2.8e-4, 512 images of 88x88x88 per step."""
+    keras.backend.clear_session()
+    reg = keras.regularizers.l2(1e-6)
+    inp = keras.Input(shape=(None, None, 88))
+    x0 = keras.layers.Conv2D(64, 1, padding='same', activation='softsign', kernel_regularizer=reg,
+                             kernel_initializer=keras.initializers.GlorotUniform())(inp)
+    x0 = keras.layers.SpatialDropout2D(1e-4)(x0)
+    x1 = keras.layers.Conv2D(3, 1, padding='same', activation='linear', kernel_regularizer=reg,
+                             kernel_initializer=keras.initializers.GlorotUniform())(x0)
+    x1 = keras.layers.SpatialDropout2D(1e-4)(x1)
+    m = keras.Model(inputs=inp, outputs=x1)
+    m.compile(optimizer=keras.optimizers.Adam(learning_rate=0.00028), loss='mse', metrics=['mae'])
+    eng = m._eng()
+    n, Pm = PER_GPU, 88 * 88
+    g = torch.Generator(device=dev)
+    g.manual_seed(88)
+    x = torch.clamp_min(0.6 * torch.randn((n * Pm, 88), generator=g, device=dev) - 0.3, 0.0).contiguous()
+    y = (20.0 * torch.randn((n, 3), generator=g, device=dev)).contiguous()
+    inv = 1.0 / (n * Pm * 3)
+    stats = torch.zeros((steps + warmup + 1, 2 + eng.optim_grid()), device=dev)
+    for i in range(warmup):
+        eng.gradient(x, y, Pm, None, n, inv, seed=i + 1)
+        eng.optimizer_step(m.optimizer, stats[i])
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    ks = []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        a0 = torch.cuda.Event(enable_timing=True)
+        a1 = torch.cuda.Event(enable_timing=True)
+        a0.record()
+        eng.gradient(x, y, Pm, None, n, inv, seed=warmup + i + 1)
+        a1.record()
+        ks.append((a0, a1))
+        eng.optimizer_step(m.optimizer, stats[warmup + i])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kms = float(np.mean([a.elapsed_time(b) for a, b in ks]))
+    flop = 2 * (88 * 64 + 64 * 3) * 2 + 2 * 64 * 3            # fwd + dW + dX(layer 2) per position
+    ach = flop * n * Pm / (kms * 1e-3)
+    return {'workload': 'Model-88 create_model (88-64 softsign-3, dropout 1e-4, l2 1e-6) training, legacy Adam, '
+                        '512 images of 88x88 feature maps',
+            'value': n / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3, 'dtype': 'fp32',
+            'kernel': eng.program('train', Pm).prog.kind + '_kernel + reduce_kernel',
+            'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': PEAK_FP32 / 1e12, 'unit': 'TFLOP/s',
+                         'frac': ach / PEAK_FP32, 'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
+
+
 BLAZE_B = 1024
 BLAZE_ID = 'reg1-stoqa9pt-reg2-hrchr82r-selected'
 
@@ -191,6 +243,7 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-infer', action='store_true')
     ap.add_argument('--no-blaze', action='store_true')
+    ap.add_argument('--no-train88', action='store_true')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -318,6 +371,9 @@ def main():
                              ie.program('fwd', P).prog.kind, '?') + ' (hpe_forward)',
                          'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
                          'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
+    # ---- Model-88 on 88x88 maps (north_star's second map size) --------------------------------
+    if rank == 0 and not a.no_train88:
+        out['train88'] = bench_train88(hpe, keras, dev, max(5, min(a.steps, 20)), 2)
     # ---- BlazeFace + both pose heads ----------------------------------
     if rank == 0 and not a.no_blaze:
         out['blazeface'] = bench_blazeface(dev, max(10, a.steps), a.no_cpu or world > 1)
