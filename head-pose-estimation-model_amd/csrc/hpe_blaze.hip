@@ -242,9 +242,242 @@ __global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// rows: the same fused block, streamed.  A workgroup owns a segment of one image's output rows
+// and walks it TH rows per step.  LDS holds W^T, the depthwise table and a ring of ROWS input
+// rows (exactly the rows one step reads); the R*S input rows the next step adds are loaded into
+// registers while this step computes (each thread's share is a contiguous run of the NHWC rows, so
+// the loads are plain coalesced float4s), and written over the ring slots this step frees.  Every
+// input byte is read from HBM once per segment: no halo tiles, no load/compute serialisation.
+// ------------------------------------------------------------------------------------------------
+#define RPF 4   // max float4 prefetched per thread per step
+
+// CINP / COUTP > 0: channel counts fixed at compile time (every LDS offset of the depthwise taps,
+// W^T rows and the epilogue becomes an immediate; the VALU work per step is then the depthwise FMAs
+// and little else).  0: read from the op words.  Wo >= 32, so a 32-position chunk is one row.
+template <int S, int NC_, int CINP, int COUTP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) bf_rows_kernel(BfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NC = COUTP ? (COUTP + 31) / 32 : NC_;
+  const int* f = a.f;
+  const int H = f[BFO_H], W = f[BFO_W], Ho = f[BFO_HO], Wo = f[BFO_WO];
+  const int Cinp = CINP ? CINP : f[BFO_CINP];
+  const int Coutp = COUTP ? COUTP : f[BFO_COUTP];
+  const int CS = CINP ? CINP + 4 : f[BFO_CS];
+  const int KS = CINP ? CINP + 4 : f[BFO_KS];
+  const int ostride = COUTP ? COUTP : f[BFO_OSTRIDE];
+  const int NCT = COUTP ? NC : f[BFO_NCT];
+  const int R = f[BFO_TH], NSEG = f[BFO_NI], RING = f[BFO_ROWS], COLS = f[BFO_COLS];
+  const int padt = f[BFO_PADT], padl = f[BFO_PADL];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int lgWo = __builtin_ctz(Wo);
+  const int nthr = blockDim.x, nwaves = nthr >> 6;
+  const float* P_ = a.params;
+  float* wt = lds;
+  float* dwt = wt + NCT * 32 * KS;
+  float* ring = dwt + 10 * Cinp;
+  const int rowLDS = COLS * CS;
+
+  const int wid = xcd_work_id(a.nwg);
+  const int64_t img = wid / NSEG;
+  const int seg = wid - (int)img * NSEG;
+  const int seg_rows = Ho / NSEG;
+  const int oy_begin = seg * seg_rows;
+  const int kq = Cinp >> 2;
+  const float* simg = a.src + img * (int64_t)H * W * Cinp;
+
+  // ---- W^T, depthwise table, zeroed ring (pad columns stay zero for the whole launch) ----
+  for (int i = threadIdx.x; i < NCT * 32 * kq; i += nthr) {
+    const int n = i / kq, q = i - n * kq;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (n < Coutp) v = ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * q);
+    *(f32x4*)(wt + n * KS + 4 * q) = v;
+  }
+  for (int i = threadIdx.x; i < 10 * kq; i += nthr) *(f32x4*)(dwt + 4 * i) = ld4(P_ + f[BFO_DWW] + 4 * i);
+  for (int i = threadIdx.x; i < RING * rowLDS / 4; i += nthr) *(f32x4*)(ring + 4 * i) = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  // ---- prologue: the first step's RING input rows straight into the ring ----
+  const int rowq = W * kq;  // float4 per input row (contiguous in HBM)
+  {
+    const int iy0 = oy_begin * S - padt;
+    for (int e = threadIdx.x; e < RING * rowq; e += nthr) {
+      const int rr = e / rowq, rem = e - rr * rowq;
+      const int ix = rem / kq, q = rem - ix * kq;
+      const int iy = iy0 + rr;
+      if (iy >= 0 && iy < H) {
+        const int slot = (iy + RING) % RING;
+        *(f32x4*)(ring + slot * rowLDS + (ix + padl) * CS + 4 * q) = ld4(simg + ((int64_t)iy * W + ix) * Cinp + 4 * q);
+      }
+    }
+  }
+  // per-thread share of a step's new rows: float4 e = t + i*nthr of the NEW contiguous rows
+  const int NEW = R * S;
+  const int newq = NEW * rowq;
+  int pf_row[RPF], pf_off[RPF];
+#pragma unroll
+  for (int i = 0; i < RPF; ++i) {
+    const int e = threadIdx.x + i * nthr;
+    const int rr = e / rowq, rem = e - rr * rowq;
+    const int ix = rem / kq, q = rem - ix * kq;
+    pf_row[i] = e < newq ? rr : -1;
+    pf_off[i] = (ix + padl) * CS + 4 * q;
+  }
+  __syncthreads();
+
+  const int ngrp = NCT / NC;
+  const int ntask = ((R * Wo) >> 5) * ngrp;
+  const int nsteps = seg_rows / R;
+
+  auto compute = [&](int oy0) {
+    for (int task = wave; task < ntask; task += nwaves) {
+      const int chunk = task / ngrp, grp = task - chunk * ngrp;
+      const int oyc = oy0 + ((chunk * 32) >> lgWo);          // the chunk's output row
+      const int x0 = (chunk * 32) & (Wo - 1);
+      int s0 = oyc * S - padt;
+      s0 = (s0 + RING) % RING;
+      const int s1 = s0 + 1 == RING ? 0 : s0 + 1;
+      const int s2 = s1 + 1 == RING ? 0 : s1 + 1;
+      const int colx = (x0 + l32) * S * CS;
+      const float* r0 = ring + s0 * rowLDS + colx;
+      const float* r1 = ring + s1 * rowLDS + colx;
+      const float* r2 = ring + s2 * rowLDS + colx;
+      const float* wb = wt + (grp * NC * 32 + l32) * KS;
+      f32x16 acc[NC];
+#pragma unroll
+      for (int nc = 0; nc < NC; ++nc) acc[nc] = (f32x16){};
+#pragma unroll 1
+      for (int c0 = 4 * half; c0 < (CINP ? CINP : Cinp); c0 += 8) {
+        f32x4 av = ld4(dwt + 9 * Cinp + c0);
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const float* rp = tp < 3 ? r0 : (tp < 6 ? r1 : r2);
+          const f32x4 xv = ld4(rp + (tp % 3) * CS + c0);
+          const f32x4 wv = ld4(dwt + tp * Cinp + c0);
+          av.x = fmaf(xv.x, wv.x, av.x);
+          av.y = fmaf(xv.y, wv.y, av.y);
+          av.z = fmaf(xv.z, wv.z, av.z);
+          av.w = fmaf(xv.w, wv.w, av.w);
+        }
+#pragma unroll
+        for (int nc = 0; nc < NC; ++nc) {
+          const f32x4 bv = ld4(wb + nc * 32 * KS + c0);
+          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[nc], 0, 0, 0);
+          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[nc], 0, 0, 0);
+          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc[nc], 0, 0, 0);
+          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc[nc], 0, 0, 0);
+        }
+      }
+      // epilogue: register g <-> position x0 + 4*half + (g&3) + 8*(g>>2) of row oyc
+      const int xh = x0 + 4 * half;
+      const float* rres;
+      const float* rres1 = nullptr;
+      if (S == 1) {
+        rres = ring + (oyc % RING) * rowLDS + (xh + padl) * CS;
+      } else {
+        rres = ring + ((2 * oyc) % RING) * rowLDS + 2 * xh * CS;
+        rres1 = ring + ((2 * oyc + 1) % RING) * rowLDS + 2 * xh * CS;
+      }
+      float* out = a.dst + ((img * Ho + oyc) * Wo + xh) * ostride;
+#pragma unroll
+      for (int nc = 0; nc < NC; ++nc) {
+        const int n = (grp * NC + nc) * 32 + l32;
+        if (n >= Coutp) continue;
+        const float bias = P_[f[BFO_PWB] + n];
+        const bool has_res = n < Cinp;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int d = (g & 3) + 8 * (g >> 2);
+          float v = acc[nc][g] + bias;
+          if (has_res) {
+            if (S == 1) {
+              v += rres[d * CS + n];
+            } else {
+              const float* t0 = rres + 2 * d * CS + n;
+              const float* t1 = rres1 + 2 * d * CS + n;
+              v += fmaxf(fmaxf(t0[0], t0[CS]), fmaxf(t1[0], t1[CS]));
+            }
+          }
+          out[d * ostride + n] = v > 0.f ? v : 0.f;
+        }
+      }
+    }
+  };
+  // first input row step j adds (rows of step j-1 plus NEW more); its NEW rows are contiguous in HBM
+  auto first_new = [&](int j) { return (oy_begin + j * R) * S - padt + (RING - NEW); };
+  auto issue = [&](f32x4 (&pf)[RPF], int j) {
+    if (j >= nsteps) return;
+    const int r0 = first_new(j);
+    const float* base = simg + (int64_t)r0 * rowq * 4 + threadIdx.x * 4;
+#pragma unroll
+    for (int i = 0; i < RPF; ++i)
+      if (pf_row[i] >= 0 && r0 + pf_row[i] < H) pf[i] = ld4(base + i * nthr * 4);
+  };
+  auto commit = [&](f32x4 (&pf)[RPF], int j) {
+    const int r0 = first_new(j);
+    const int slot0 = (r0 + RING) % RING;
+#pragma unroll
+    for (int i = 0; i < RPF; ++i) {
+      if (pf_row[i] < 0) continue;
+      int sl = slot0 + pf_row[i];
+      sl -= sl >= RING ? RING : 0;
+      const f32x4 v = r0 + pf_row[i] < H ? pf[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      *(f32x4*)(ring + sl * rowLDS + pf_off[i]) = v;
+    }
+  };
+  // three steps of rows in flight per workgroup
+  f32x4 pa[RPF], pb[RPF], pc[RPF];
+  issue(pa, 1);
+  issue(pb, 2);
+  issue(pc, 3);
+  for (int k = 0; k < nsteps; k += 3) {
+    compute(oy_begin + k * R);
+    __syncthreads();
+    if (k + 1 >= nsteps) break;
+    commit(pa, k + 1);
+    issue(pa, k + 4);
+    __syncthreads();
+    compute(oy_begin + (k + 1) * R);
+    __syncthreads();
+    if (k + 2 >= nsteps) break;
+    commit(pb, k + 2);
+    issue(pb, k + 5);
+    __syncthreads();
+    compute(oy_begin + (k + 2) * R);
+    __syncthreads();
+    if (k + 3 >= nsteps) break;
+    commit(pc, k + 3);
+    issue(pc, k + 6);
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
 typedef void (*bf_fn)(BfArgs);
+
+// compile-time channel specialisations of the BlazeFace 64x64 / 32x32 stages (CS = KS = CINP + 4,
+// output stride COUTP, all output-channel chunks in one task); anything else runs the generic one
+static bf_fn pick_rows(int s, int nc, int cinp = 0, int coutp = 0, int cs = 0, int ks = 0, int ostride = 0, int nct = 0) {
+  if (cs == cinp + 4 && ks == cinp + 4 && ostride == coutp && nct == (coutp + 31) / 32 && nc == nct) {
+#define BF_ROWS_T(S_, CI_, CO_) if (s == S_ && cinp == CI_ && coutp == CO_) return bf_rows_kernel<S_, 0, CI_, CO_>;
+    BF_ROWS_T(1, 24, 24)
+    BF_ROWS_T(1, 24, 32)
+    BF_ROWS_T(2, 32, 32)
+    BF_ROWS_T(1, 32, 40)
+    BF_ROWS_T(1, 40, 48)
+    BF_ROWS_T(2, 48, 48)
+#undef BF_ROWS_T
+  }
+  if (s == 1 && nc == 1) return bf_rows_kernel<1, 1, 0, 0>;
+  if (s == 1 && nc == 2) return bf_rows_kernel<1, 2, 0, 0>;
+  if (s == 2 && nc == 1) return bf_rows_kernel<2, 1, 0, 0>;
+  if (s == 2 && nc == 2) return bf_rows_kernel<2, 2, 0, 0>;
+  return nullptr;
+}
+static bf_fn pick_rows_op(const int* f) {
+  return pick_rows(f[BFO_STRIDE], f[BFO_NC], f[BFO_CINP], f[BFO_COUTP], f[BFO_CS], f[BFO_KS], f[BFO_OSTRIDE], f[BFO_NCT]);
+}
 
 static bf_fn pick_block(int s, int dw, int nc) {
 #define BF_NC(S_, DW_)                                   \
@@ -271,7 +504,28 @@ struct hpe_blazeface {
 
 static int check_op(const int* f, int i) {
   const int kind = f[BFO_KIND];
-  if (kind != BF_STEM && kind != BF_BLOCK) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
+  if (kind != BF_STEM && kind != BF_BLOCK && kind != BF_ROWS) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
+  if (kind == BF_ROWS) {
+    const int S = f[BFO_STRIDE], R = f[BFO_TH], nseg = f[BFO_NI], kq = f[BFO_CINP] / 4;
+    if (!pick_rows_op(f) || !f[BFO_DW] || f[BFO_SPLIT] || !f[BFO_RELU]) return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel variant", i);
+    if (f[BFO_WAVES] < 1 || f[BFO_WAVES] > 4) return hpe_fail(HPE_EINVAL, "blazeface op %d: waves", i);
+    if (R <= 0 || nseg <= 0 || f[BFO_HO] % nseg || (f[BFO_HO] / nseg) % R) return hpe_fail(HPE_EINVAL, "blazeface op %d: row steps", i);
+    const int wo = f[BFO_WO];
+    if (wo < 32 || (wo & (wo - 1)) || (R * wo) % 32) return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel needs Wo >= 32, a power of two", i);
+    if (f[BFO_ROWS] != (R - 1) * S + 3 || f[BFO_COLS] != (wo - 1) * S + 3) return hpe_fail(HPE_EINVAL, "blazeface op %d: ring geometry", i);
+    if (S == 1 ? (f[BFO_PADT] != 1 || f[BFO_PADL] != 1 || f[BFO_RES] != BF_RES_ID || f[BFO_H] != f[BFO_HO] || f[BFO_W] != wo)
+               : (f[BFO_PADT] || f[BFO_PADL] || f[BFO_RES] != BF_RES_MAXPOOL || f[BFO_H] != 2 * f[BFO_HO] || f[BFO_W] != 2 * wo))
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel stride/padding/residual", i);
+    if (R * S * f[BFO_W] * kq > RPF * 64 * f[BFO_WAVES]) return hpe_fail(HPE_EINVAL, "blazeface op %d: prefetch share exceeds %d float4/thread", i, RPF);
+    if (f[BFO_CINP] % 8 || f[BFO_CS] < f[BFO_CINP] || f[BFO_CS] % 4 || f[BFO_KS] < f[BFO_CINP] || f[BFO_KS] % 4 ||
+        f[BFO_NCT] < 1 || f[BFO_NCT] * 32 < f[BFO_COUTP] || f[BFO_NCT] % f[BFO_NC] || f[BFO_OSTRIDE] < f[BFO_COUT] ||
+        f[BFO_OSTRIDE] > f[BFO_COUTP] || f[BFO_COUTP] % 8)
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: channel geometry", i);
+    const long need = 4L * (f[BFO_NCT] * 32 * f[BFO_KS] + 10 * f[BFO_CINP] + (long)f[BFO_ROWS] * f[BFO_COLS] * f[BFO_CS]);
+    if (f[BFO_LDS] < need || f[BFO_LDS] > 160 * 1024) return hpe_fail(HPE_EINVAL, "blazeface op %d: LDS", i);
+    if (f[BFO_SRC] < 0 || f[BFO_SRC] >= BF_NBUF || f[BFO_DST] < 0 || f[BFO_DST] >= BF_NBUF) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad buffer", i);
+    return 0;
+  }
   if (f[BFO_TH] <= 0 || f[BFO_NI] <= 0 || f[BFO_HO] % f[BFO_TH]) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad tile", i);
   if ((f[BFO_NI] * f[BFO_TH] * f[BFO_WO]) % 32) return hpe_fail(HPE_EINVAL, "blazeface op %d: tile not a multiple of 32 positions", i);
   if (f[BFO_NI] > 1 && f[BFO_TH] != f[BFO_HO]) return hpe_fail(HPE_EINVAL, "blazeface op %d: multi-image tiles must be whole images", i);
@@ -367,11 +621,14 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
     a.dst2 = f[BFO_SPLIT] ? bufs[f[BFO_DST2]] : nullptr;
     a.nimg = n_images;
     const int64_t tpi = f[BFO_HO] / f[BFO_TH];
-    const int64_t nwg = f[BFO_NI] > 1 ? (n_images + f[BFO_NI] - 1) / f[BFO_NI] : n_images * tpi;
+    const int64_t nwg = f[BFO_KIND] == BF_ROWS ? n_images * f[BFO_NI]
+                        : f[BFO_NI] > 1 ? (n_images + f[BFO_NI] - 1) / f[BFO_NI] : n_images * tpi;
     if (nwg > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
     a.nwg = (int)nwg;
     const int threads = 64 * f[BFO_WAVES];
-    bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
+    bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel
+              : f[BFO_KIND] == BF_ROWS ? pick_rows_op(f)
+                                       : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(threads), f[BFO_LDS], s, a);
     const hipError_t e = hipGetLastError();

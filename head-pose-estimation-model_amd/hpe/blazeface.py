@@ -24,7 +24,8 @@ from . import _lib
 BF_MAGIC = 0x46425048
 BFH_WORDS = 8
 (BFH_MAGIC, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF) = range(4)
-BF_STEM, BF_BLOCK = 1, 2
+BF_STEM, BF_BLOCK, BF_ROWS = 1, 2, 3
+ROWS_PF = 4                 # float4 per thread the rows kernel prefetches per step (csrc RPF)
 RES_NONE, RES_ID, RES_MAXPOOL = 0, 1, 2
 BUF_IMG, BUF_A, BUF_B, BUF_OUT0 = 0, 1, 2, 3
 (BFO_KIND, BFO_H, BFO_W, BFO_HO, BFO_WO, BFO_CIN, BFO_COUT, BFO_CINP, BFO_COUTP,
@@ -242,6 +243,27 @@ def _block_tile(ho, wo, s, dw, cinp, nct, ks, cs):
     return best[1:]
 
 
+def _rows_plan(bl, cinp, nct, ks, cs):
+    """Row-streaming variant for the large maps: steps of R output rows (R*Wo = 128 positions
+    when the per-thread prefetch share allows), 4 waves, NSEG segments per image."""
+    s, wo, w, ho = bl['stride'], bl['Wo'], bl['W'], bl['Ho']
+    kq = cinp // 4
+    for r in (128 // wo, 64 // wo, 32 // wo):
+        if r < 1 or ho % r or (r * wo) % 32:
+            continue
+        if r * s * w * kq > ROWS_PF * 256:
+            continue
+        ring, cols = (r - 1) * s + 3, (wo - 1) * s + 3
+        nc = nct if nct <= 2 else 1
+        lds = 4 * (nct * 32 * ks + 10 * cinp + ring * cols * cs)
+        if lds > 160 * 1024:
+            continue
+        steps = ho // r
+        nseg = 2 if steps % 2 == 0 and steps >= 8 else 1
+        return r, nseg, ring, cols, lds, nc, 4
+    return None
+
+
 def build_plan(model_config, weights):
     st = parse(model_config)
     P = _Params()
@@ -302,7 +324,11 @@ def build_plan(model_config, weights):
         nct = -(-coutp // 32)
         s = bl['stride']
         cs = ks = cinp + 4                                    # (cs/4) odd: conflict-free b128 rows
-        th, ni, rows, cols, lds, nc, waves = _block_tile(bl['Ho'], bl['Wo'], s, True, cinp, nct, ks, cs)
+        rows_plan = _rows_plan(bl, cinp, nct, ks, cs) if bl['Wo'] >= 32 else None
+        if rows_plan:
+            th, ni, rows, cols, lds, nc, waves = rows_plan
+        else:
+            th, ni, rows, cols, lds, nc, waves = _block_tile(bl['Ho'], bl['Wo'], s, True, cinp, nct, ks, cs)
         if bl['out'] in tap_buf:
             dst = tap_buf[bl['out']]
             if coutp != cout:
@@ -310,7 +336,8 @@ def build_plan(model_config, weights):
         else:
             dst = BUF_B if cur_buf == BUF_A else BUF_A
         f = [0] * BFO_WORDS
-        f[BFO_KIND], f[BFO_H], f[BFO_W], f[BFO_HO], f[BFO_WO] = BF_BLOCK, bl['H'], bl['W'], bl['Ho'], bl['Wo']
+        f[BFO_KIND] = BF_ROWS if rows_plan else BF_BLOCK
+        f[BFO_H], f[BFO_W], f[BFO_HO], f[BFO_WO] = bl['H'], bl['W'], bl['Ho'], bl['Wo']
         f[BFO_CIN], f[BFO_COUT], f[BFO_CINP], f[BFO_COUTP] = cin, cout, cinp, coutp
         f[BFO_STRIDE] = s
         f[BFO_PADT], f[BFO_PADL] = (1, 1) if s == 1 else (0, 0)
