@@ -145,7 +145,7 @@ def bench_train88(hpe, keras, dev, steps, warmup):
             'value': n / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3, 'dtype': 'fp32',
             'kernel': eng.program('train', Pm).prog.kind + '_kernel + reduce_kernel',
             'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': PEAK_FP32 / 1e12, 'unit': 'TFLOP/s',
-                         'frac': ach / PEAK_FP32, 'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
+                         'frac': ach / PEAK_FP32, 'traffic': _traffic('train88'), 'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
 
 
 BLAZE_B = 1024

@@ -9,6 +9,7 @@ coalesced 16-B/lane stream -> bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE exact fo
 1024 * WRITE_SIZE.  Only dispatches of the bench's timed kernels are averaged.
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -37,26 +38,36 @@ def main(tag):
     write = counters(os.path.join(OUT, 'prof_write', 'write_counter_collection.csv'), 'WRITE_SIZE')
     rows = []
     res = {}
+    per = {}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])
         w = write.get(k, [])
         fb = 2 * 1024 * sum(f) / len(f) if f else 0.0
         wb = 1024 * sum(w) / len(w) if w else 0.0
         rows.append((k[:120], len(f), fb, wb, fb + wb))
-        short = k.split('(')[0]
-        if short.startswith('void mlp2_kernel') or (short.startswith('void rowprog_kernel') and 'train' not in res and fb > 5e8):
-            res.setdefault('train', {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb,
-                                     'hbm_bytes_per_launch': fb + wb})
-    # infer: the forward launches of bench's infer line (hrchr82r, 256 x 96x96 rows of 96 fp32)
-    for k in sorted(fetch):
-        short = k.split('(')[0]
-        f = fetch[k]
-        w = write.get(k, [0])
-        if 'rowprog_kernel<4' in short or 'chain_fwd' in short:
-            fb = 2 * 1024 * sum(f) / len(f)
-            wb = 1024 * sum(w) / len(w)
-            res['infer'] = {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb,
-                            'hbm_bytes_per_launch': fb + wb}
+        per[k.split('(')[0]] = (fb, wb, len(f))
+
+    def put(key, short):
+        fb, wb, _ = per[short]
+        res[key] = {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb, 'hbm_bytes_per_launch': fb + wb}
+
+    # bench lines -> their dominant kernels (template args: <KH, RBW, ACT1, DROP>; ACT 1 = tanh, 3 = softsign)
+    for short in per:
+        if short.startswith('void mlp2_kernel<48') and short.endswith('false>'):
+            put('train', short)
+        elif short.startswith('void mlp2_kernel<44') and short.endswith('true>'):
+            put('train88', short)
+        elif 'chain_fwd' in short:
+            put('infer', short)
+    # BlazeFace forward = every bf_* launch of one forward (one dispatch each per forward per kernel
+    # name, except the 64x64/32x32 block kernels that run several blocks): bytes per forward
+    bf = [(s, v) for s, v in per.items() if re.match(r'(void )?bf_', s)]
+    if bf:
+        nfwd = min(v[2] for s, v in bf if 'stem' in s) if any('stem' in s for s, _ in bf) else 1
+        tot_f = sum(v[0] * v[2] for _, v in bf) / nfwd
+        tot_w = sum(v[1] * v[2] for _, v in bf) / nfwd
+        res['blazeface'] = {'kernel': 'bf_* (one forward)', 'fetch_bytes': tot_f, 'write_bytes': tot_w,
+                            'hbm_bytes_per_launch': tot_f + tot_w}
     with open(os.path.join(PROF, '%s_traffic.csv' % tag), 'w') as fh:
         wr = csv.writer(fh)
         wr.writerow(['kernel', 'dispatches', 'fetch_bytes_per_launch(x2 gfx950)', 'write_bytes_per_launch', 'hbm_bytes_per_launch'])
