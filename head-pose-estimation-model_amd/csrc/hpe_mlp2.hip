@@ -21,15 +21,51 @@
 
 #include "hpe_common.h"
 
-#define MLP2_MAXW 12  // waves per workgroup (hidden width <= 384)
+#define MLP2_MAXW 12          // waves per workgroup (hidden width <= 384)
+#define MLP2_XS 100             // LDS row stride of an X tile (floats): conflict-free, 16-B aligned
+#define MLP2_XF (32 * MLP2_XS)  // floats per X tile buffer
+#define MLP2_LAB 128            // floats per label buffer: [32 rows][4] (yaw, pitch, roll, pad)
 
-static __device__ __forceinline__ int ceil8(int c) { return (c + 7) & ~7; }
-static __device__ __forceinline__ int xstride(int cp) { return ((cp >> 2) & 1) ? cp : cp + 4; }
+// LDS-DMA (global_load_lds) in inline asm: hipcc's waitcnt pass cannot tell the two X buffers
+// apart and would put vmcnt(0) before every ds_read of the tile in use, draining the prefetch of
+// the next one; hidden from it, the prefetch completes only at the explicit vmcnt(0) before the
+// barrier that opens its tile.  M0 is written in the same statement (compiler-reserved).
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p);
+}
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+// raw workgroup barrier that waits for LDS traffic only: an in-flight global_load_lds prefetch of
+// the next tile survives it (__syncthreads() would drain it with vmcnt(0))
+__device__ __forceinline__ void bar_lds() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
 
 struct E2 {
   int act, drop;
   uint32_t thr;
   float keep;
+};
+
+// image of tile row r: tile = rows [row0, row0 + 32) with row0 = img0 * P + rem0 (no 64-bit
+// division per row; at P >= 32 a tile straddles at most one image boundary)
+struct TileImg {
+  int64_t img0;
+  int rem0, P;
+  __device__ __forceinline__ int64_t of(int r) const {
+    const int t = rem0 + r;
+    return img0 + (P >= 32 ? (t >= P ? 1 : 0) : (P == 1 ? t : t / P));
+  }
 };
 
 __device__ __forceinline__ float e_fwd(const E2& e, uint64_t seed, int64_t img, int ch, float z) {
@@ -62,37 +98,78 @@ __device__ __forceinline__ float act1_f(int act, float z) {
   if (ACT1 == ACT_SOFTSIGN) return z * __builtin_amdgcn_rcpf(1.f + fabsf(z));
   return act_f(ACT1 >= 0 ? ACT1 : act, z);
 }
-
-// image index of tile row r (dropout hash); P == 1 (the reference's 1x1 layout) needs no division
-__device__ __forceinline__ uint64_t row_image(int64_t row0, int r, int P, int64_t off) {
-  return (uint64_t)((P == 1 ? row0 + r : (row0 + r) / P) + off);
-}
 template <int ACT1>
 __device__ __forceinline__ float act1_g(int act, float a) {
   const int k = ACT1 >= 0 ? ACT1 : act;
   return k == ACT_LINEAR ? 1.f : act_grad(k, a, 0.f);
 }
 
-template <int KH, int RBW, int ACT1, bool DROP>
-__global__ void __launch_bounds__(MLP2_MAXW * 64) mlp2_kernel(Args args) {
+// HBM -> LDS staging of one 32-row tile: one global_load_lds_dwordx4 per row with C_in/4 lanes
+// active (lane i -> 16 B at the row's padded LDS base + 16 i), rows shared round-robin by the
+// workgroup's waves; rows past the end repeat the last row (their loss gradient is zero).  The
+// labels of the tile's rows for the loss: 2 x 64 dwords by wave 0.  Gather mode (fit's shuffled
+// batches): lane l looks up the source image of tile row l once, before any piece is issued, so
+// the only wait in here never drains an in-flight prefetch.
+__device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* lab, int64_t row0,
+                                           int wave, int NCB, int lane, int Cin, bool labels) {
+  const int64_t nrows = args.nrows;
+  const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
+  const int P = args.P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = row0 / P;
+  ti.rem0 = (int)(row0 - ti.img0 * P);
+  const int lr = min(lane & 31, last);
+  const int64_t limg = ti.of(lr);
+  const int lpos = (int)(row0 + lr - limg * P);
+  const int64_t lsrc = args.idx ? (int64_t)args.idx[limg] : limg;  // source image of tile row lr
+  // retire the index load here, visibly to hipcc's waitcnt pass (vmcnt(0)): otherwise it waits
+  // for it (and so for every LDS-DMA piece issued below) at the next reuse of its register
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (labels && wave == 0) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int slot = pc * 64 + lane;
+      const int r = min(slot >> 2, last), j = min(slot & 3, 2);
+      const int64_t src = (int64_t)__shfl((int)lsrc, r, 64);
+      glds4(args.ytrue + src * 3 + j, lds_addr(lab + pc * 64));
+    }
+  }
+  const int q = Cin >> 2;
+  for (int r = wave; r < 32; r += NCB) {
+    const int rr = min(r, last);
+    const int64_t srow = (int64_t)__builtin_amdgcn_readlane((int)lsrc, rr) * P +
+                         __builtin_amdgcn_readlane(lpos, rr);
+    if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
+  }
+}
+
+// NWM: launch bound in waves (12: any width <= 384, 168-VGPR budget; 4: F <= 128, 256 budget)
+template <int KH, int ACT1, bool DROP, int NWM>
+__global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NKB = (2 * KH + 31) / 32;  // 32-row blocks of dW1 (input channels)
-  constexpr int T = 32 * RBW;
+  constexpr int T = 32;
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int mode = prog[H_MODE];
   const bool train = mode == MODE_TRAIN;
   const int Cin = o[O_K], F = o[O_N], NCB = o[O_MODE];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
   const int NT = blockDim.x;
   const int n = wave * 32 + l32;
   const bool nok = n < F;
-  const int cp = ceil8(Cin), Kh = cp >> 1, xst = xstride(cp);
-  // LDS: X tile [T][xst] | head partials [NCB][T][4] | dZ2 [T][4] | reduction scratch
-  float* xs = lds;
-  float* part = lds + T * xst;
+  // LDS: X tiles [2][32][MLP2_XS] | labels [2][128] | head partials [NCB][T][4] | dZ2 [T][4] | scratch
+  float* xbuf = lds;
+  float* lbuf = xbuf + 2 * MLP2_XF;
+  float* part = lbuf + 2 * MLP2_LAB;
   float* dz2 = part + NCB * T * 4;
-  float* red = dz2 + T * 4;
+  float* a1s = dz2 + T * 4;       // [NCB][16][64]: layer-1 activations, forward -> backward
+  float* w2t = a1s + NCB * 1024;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
+  float* b2t = w2t + NCB * 128;
+  float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
+  float* red = hacc + NCB * 256;  // [NCB * 64]
 
   E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
   E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
@@ -104,195 +181,220 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) mlp2_kernel(Args args) {
   float wreg[KH];
 #pragma unroll
   for (int m = 0; m < KH; ++m) {
-    const int k = half * Kh + m;  // KH == ceil8(C_in)/2
+    const int k = half * KH + m;
     const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
     wreg[m] = (k < Cin && nok) ? wv : 0.f;
   }
   const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
-  float w2[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) w2[j] = nok ? W2[n * 3 + j] : 0.f;
-  float b2[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) b2[j] = o[O_AUX1] >= 0 ? args.params[o[O_AUX1] + j] : 0.f;
+  // small tables in LDS rather than loop-carried VGPRs (the 12-wave variant is at its budget)
+  for (int i = threadIdx.x; i < NCB * 128; i += NT) {
+    const int nn = i >> 2, j = i & 3;
+    w2t[i] = (nn < F && j < 3) ? W2[nn * 3 + j] : 0.f;
+  }
+  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
+  for (int i = threadIdx.x; i < NT * 4; i += NT) hacc[i] = 0.f;
 
   f32x16 dw[NKB];
 #pragma unroll
   for (int s = 0; s < NKB; ++s) dw[s] = f32x16{};
   float dw2[3] = {0.f, 0.f, 0.f};
-  float db1 = 0.f, db2acc = 0.f, sse = 0.f, sae = 0.f;
+  float db1 = 0.f;
 
   const int64_t nrows = args.nrows;
   const int64_t ntiles = (nrows + T - 1) / T;
   const int P = args.P;
-  const int q = Cin >> 2, qp = cp >> 2;
+  const bool labels = mode != MODE_FWD;
+  // head phase: thread it handles (row, output) items it, it + NT3, ... with NT3 a multiple of 3,
+  // so its output index j (and its db2 accumulator) is the same in every tile
+  const int NT3 = (NT / 3) * 3;
 
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t row0 = tile * T;
-    // ---- stage X rows (16-B coalesced loads; padding columns written as zero) ----
-    for (int it = threadIdx.x; it < T * qp; it += NT) {
-      const int r = it / qp, jq = it - r * qp;
-      const int64_t R = row0 + r;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (R < nrows && jq < q) {
-        const int64_t img = R / P, pos = R - img * P;
-        const int64_t src = (args.idx ? (int64_t)args.idx[img] : img) * P + pos;
-        v = *(const f32x4*)(args.x + src * Cin + 4 * jq);
-      }
-      *(f32x4*)(xs + r * xst + 4 * jq) = v;
+  // pad columns [C_in, ceil8(C_in)) of both X buffers: never written by the staging, read by the
+  // forward MFMA against zero weights -> must hold zeros, not stale LDS
+  for (int i = threadIdx.x; i < 64 * 8; i += NT) {
+    const int r = i >> 3, c = Cin + (i & 7);
+    if (c < ((Cin + 7) & ~7)) xbuf[r * MLP2_XS + c] = 0.f;
+  }
+  __syncthreads();
+  if (blockIdx.x < ntiles) {
+    stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, wave, NCB, lane, Cin, labels);
+  }
+  int buf = 0;
+  for (int tile = blockIdx.x; tile < (int)ntiles; tile += gridDim.x, buf ^= 1) {
+    const int64_t row0 = (int64_t)tile * T;
+    const float* xs = xbuf + buf * MLP2_XF;
+    const float* lab = lbuf + buf * MLP2_LAB;
+    TileImg ti;
+    ti.P = P;
+    ti.img0 = row0 / P;
+    ti.rem0 = (int)(row0 - ti.img0 * P);
+    // tile `tile` landed (own pieces) -> barrier: every wave's pieces landed, and every wave is
+    // done with tile - gridDim.x, whose buffer the prefetch below overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar_lds();
+    if (tile + gridDim.x < ntiles) {
+      stage_tile(args, xbuf + (buf ^ 1) * MLP2_XF, lbuf + (buf ^ 1) * MLP2_LAB,
+                 (int64_t)(tile + gridDim.x) * T, wave, NCB, lane, Cin, labels);
     }
-    __syncthreads();
 
     // ---- forward: Z1 = X.W1 (+b1, act, dropout) and the head partials ----
-    f32x16 a1[RBW];
+    uint32_t dmask = 0;  // layer-1 dropout keep bits of this lane's 16 rows (reused by backward)
+    {
+      const float* ap = xs + l32 * MLP2_XS + half * KH;
+      f32x16 acc = {};
+      f32x4 an = *(const f32x4*)(ap);
 #pragma unroll
-    for (int rb = 0; rb < RBW; ++rb) {
-      if (wave < NCB) {
-        const float* ap = xs + (rb * 32 + l32) * xst + half * KH;
-        f32x16 acc = {};
-        // software-pipelined: the next 4-k group's ds_read_b128 is in flight under this group's
-        // 4 MFMAs; sched_barrier keeps hipcc from hoisting every load (register budget 168)
-        f32x4 an = *(const f32x4*)(ap);
+      for (int m = 0; m < KH; m += 4) {
+        const f32x4 a = an;
+        if (m + 4 < KH) an = *(const f32x4*)(ap + m + 4);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wreg[m + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wreg[m + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wreg[m + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wreg[m + 3], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (DROP) {
+        if (P >= 32) {  // two images at most: two hashes per lane per tile
+          const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
+          const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
 #pragma unroll
-        for (int m = 0; m < KH; m += 4) {
-          const f32x4 a = an;
-          if (m + 4 < KH) an = *(const f32x4*)(ap + m + 4);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wreg[m + 0], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wreg[m + 1], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wreg[m + 2], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wreg[m + 3], acc, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          float z = act1_f<ACT1>(e1.act, acc[g] + b1);
-          if (DROP) {
-            const int r = rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-            z = drop_hash(args.seed, e1.drop, row_image(row0, r, P, args.img_off), n) >= e1.thr
-                    ? z * inv_keep1 : 0.f;
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << g) : 0u;
           }
-          acc[g] = nok ? z : 0.f;
-        }
-        a1[rb] = acc;
-        // head partials: per output j, reduce-scatter the 16 row values over the 32 lanes of a
-        // half (offsets 16, 8, 4, 2 halve the vector; xor 1 completes) -> lane holds row
-        // g = (lane >> 1) & 15 of this half
-        const int gsel = (lane >> 1) & 15;
-        const int rsel = rb * 32 + (gsel & 3) + 8 * (gsel >> 2) + 4 * half;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          float v[16];
-#pragma unroll
-          for (int g = 0; g < 16; ++g) v[g] = acc[g] * w2[j];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const bool up = lane & 16;
-            const float snd = up ? v[i] : v[i + 8];
-            v[i] = (up ? v[i + 8] : v[i]) + __shfl_xor(snd, 16, 64);
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask |= drop_hash(args.seed, e1.drop, (uint64_t)(ti.of(r) + args.img_off), n) >= e1.thr
+                         ? (1u << g) : 0u;
           }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bool up = lane & 8;
-            const float snd = up ? v[i] : v[i + 4];
-            v[i] = (up ? v[i + 4] : v[i]) + __shfl_xor(snd, 8, 64);
-          }
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const bool up = lane & 4;
-            const float snd = up ? v[i] : v[i + 2];
-            v[i] = (up ? v[i + 2] : v[i]) + __shfl_xor(snd, 4, 64);
-          }
-          {
-            const bool up = lane & 2;
-            const float snd = up ? v[0] : v[1];
-            v[0] = (up ? v[1] : v[0]) + __shfl_xor(snd, 2, 64);
-          }
-          v[0] += __shfl_xor(v[0], 1, 64);
-          if ((lane & 1) == 0) part[(wave * T + rsel) * 4 + j] = v[0];
         }
       }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        float z = act1_f<ACT1>(e1.act, acc[g] + b1);
+        if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
+        acc[g] = nok ? z : 0.f;
+      }
+      // park A1 in LDS across the head phase (16 VGPRs fewer live through the loss epilogue)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) a1s[(wave * 16 + g) * 64 + lane] = acc[g];
+      // head partials: per output j, reduce-scatter the 16 row values over the 32 lanes of a
+      // half (offsets 16, 8, 4, 2 halve the vector; xor 1 completes) -> lane holds row
+      // g = (lane >> 1) & 15 of this half
+      const int gsel = (lane >> 1) & 15;
+      const int rsel = (gsel & 3) + 8 * (gsel >> 2) + 4 * half;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        float v[16];
+        const float w2j = w2t[n * 4 + j];
+#pragma unroll
+        for (int g = 0; g < 16; ++g) v[g] = acc[g] * w2j;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool up = lane & 16;
+          const float snd = up ? v[i] : v[i + 8];
+          v[i] = (up ? v[i + 8] : v[i]) + __shfl_xor(snd, 16, 64);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool up = lane & 8;
+          const float snd = up ? v[i] : v[i + 4];
+          v[i] = (up ? v[i + 4] : v[i]) + __shfl_xor(snd, 8, 64);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool up = lane & 4;
+          const float snd = up ? v[i] : v[i + 2];
+          v[i] = (up ? v[i + 2] : v[i]) + __shfl_xor(snd, 4, 64);
+        }
+        {
+          const bool up = lane & 2;
+          const float snd = up ? v[0] : v[1];
+          v[0] = (up ? v[1] : v[0]) + __shfl_xor(snd, 2, 64);
+        }
+        v[0] += __shfl_xor(v[0], 1, 64);
+        if ((lane & 1) == 0) part[(wave * T + rsel) * 4 + j] = v[0];
+      }
     }
-    __syncthreads();
+    bar_lds();
 
     // ---- head: sum partials (fixed wave order) + b2, epilogue, loss / output ----
-    for (int it = threadIdx.x; it < T * 3; it += NT) {
+    for (int it = threadIdx.x; it < T * 3 && threadIdx.x < NT3; it += NT3) {
       const int r = it / 3, j = it - r * 3;
       const int64_t R = row0 + r;
-      float z = b2[j];
+      float z = b2t[j];
       for (int w = 0; w < NCB; ++w) z += part[(w * T + r) * 4 + j];
-      const int64_t img = R / P;
-      const float p = e_fwd(e2, args.seed, img + args.img_off, j, z);
+      const int64_t img = ti.of(r) + args.img_off;
+      // ACT1 >= 0 kernels are only picked for a linear head (the create_model family)
+      const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr
+                                                      ? z / e2.keep : 0.f) : z)
+                                : e_fwd(e2, args.seed, img, j, z);
       if (mode == MODE_FWD) {
         if (R < nrows) args.y[R * 3 + j] = p;
       } else {
         float g = 0.f;
         if (R < nrows) {
-          const int64_t src = args.idx ? (int64_t)args.idx[img] : img;
-          const float err = p - args.ytrue[src * 3 + j];
-          sse = fmaf(err, err, sse);
-          sae += fabsf(err);
+          const float err = p - lab[r * 4 + j];
+          hacc[threadIdx.x * 4 + 0] = fmaf(err, err, hacc[threadIdx.x * 4 + 0]);
+          hacc[threadIdx.x * 4 + 1] += fabsf(err);
           g = 2.f * err * args.inv_count;
         }
         if (train) {
-          g = e_bwd(e2, args.seed, img + args.img_off, j, g, p);
+          g = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr
+                                               ? g / e2.keep : 0.f) : g)
+                        : e_bwd(e2, args.seed, img, j, g, p);
           dz2[r * 4 + j] = g;
-          db2acc += g;
+          hacc[threadIdx.x * 4 + 2] += g;
         }
       }
     }
-    if (!train) {
-      __syncthreads();  // part/xs reuse by the next tile
-      continue;
-    }
-    __syncthreads();
+    if (!train) continue;  // the next tile's first barrier orders part / lab reuse
+    bar_lds();
 
     // ---- backward: dA1 = dZ2.W2^T, dZ1, dW2, db1 in registers; dW1 += X^T.dZ1 on MFMA ----
-    if (wave < NCB) {
+    {
+      float dz1[16];
+      const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
 #pragma unroll
-      for (int rb = 0; rb < RBW; ++rb) {
-        float dz1[16];
+      for (int g = 0; g < 16; ++g) {
+        const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+        const f32x4 d = *(const f32x4*)(dz2 + r * 4);
+        const float a = a1s[(wave * 16 + g) * 64 + lane];
+        const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
+        float gz, av = a;
+        if (DROP) {
+          gz = (dmask >> g) & 1u ? da * inv_keep1 : 0.f;
+          av = a * e1.keep;
+        } else {
+          gz = da;
+        }
+        gz = nok ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
+        dw2[0] = fmaf(a, d.x, dw2[0]);
+        dw2[1] = fmaf(a, d.y, dw2[1]);
+        dw2[2] = fmaf(a, d.z, dw2[2]);
+        db1 += gz;
+        dz1[g] = gz;
+        if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the dZ2 reads in flight
+      }
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        // X^T block: lane reads X[r(g)][k = 32 kb + l32]
+        const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
+        f32x16 acc = dw[kb];
+        auto xat = [&](int g) { return xp[((g & 3) + 8 * (g >> 2)) * MLP2_XS]; };
+        float x0 = xat(0), x1 = xat(1);
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          const int r = rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-          const f32x4 d = *(const f32x4*)(dz2 + r * 4);
-          const float a = a1[rb][g];
-          const float da = d.x * w2[0] + d.y * w2[1] + d.z * w2[2];
-          float gz, av = a;
-          if (DROP) {
-            const bool keep = drop_hash(args.seed, e1.drop, row_image(row0, r, P, args.img_off),
-                                        n) >= e1.thr;
-            gz = keep ? da * inv_keep1 : 0.f;
-            av = a * e1.keep;
-          } else {
-            gz = da;
-          }
-          gz = nok ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
-          dw2[0] = fmaf(a, d.x, dw2[0]);
-          dw2[1] = fmaf(a, d.y, dw2[1]);
-          dw2[2] = fmaf(a, d.z, dw2[2]);
-          db1 += gz;
-          dz1[g] = gz;
-          if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the dZ2 reads in flight
+          const float xv = x0;
+          x0 = x1;
+          if (g + 2 < 16) x1 = xat(g + 2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, dz1[g], acc, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          const float* xp = xs + (rb * 32 + 4 * half) * xst + kb * 32 + l32;
-          f32x16 acc = dw[kb];
-          // rows R(g) = (g&3) + 8(g>>2): two X reads in flight ahead of the MFMA chain
-          float x0 = xp[0], x1 = xp[1 * xst];
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const float xv = x0;
-            x0 = x1;
-            if (g + 2 < 16) x1 = xp[(((g + 2) & 3) + 8 * ((g + 2) >> 2)) * xst];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, dz1[g], acc, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          dw[kb] = acc;
-        }
+        dw[kb] = acc;
       }
     }
-    __syncthreads();
   }
 
   if (mode == MODE_FWD) return;
@@ -300,37 +402,34 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) mlp2_kernel(Args args) {
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
+  __syncthreads();
   if (train) {
-    if (wave < NCB) {
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-          if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g];
-        }
-      }
-      const float tb = db1 + __shfl_xor(db1, 32, 64);
-      float t2[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
-      if (half == 0 && nok) {
-        if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j];
+      for (int g = 0; g < 16; ++g) {
+        const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g];
       }
     }
-    // db2: per-thread (row, j) accumulators -> fixed-order sum
-    red[threadIdx.x] = threadIdx.x < T * 3 ? db2acc : 0.f;
-    __syncthreads();
+    const float tb = db1 + __shfl_xor(db1, 32, 64);
+    float t2[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
+    if (half == 0 && nok) {
+      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j];
+    }
+    // db2: per-thread accumulators of output j = tid % 3 -> fixed-order sum
     if (threadIdx.x < 3 && o[O_AUX1] >= 0) {
       float s = 0.f;
-      for (int r = 0; r < T; ++r) s += red[r * 3 + threadIdx.x];
+      for (int i = threadIdx.x; i < NT3; i += 3) s += hacc[i * 4 + 2];
       ws[o[O_AUX1] + threadIdx.x] = s;
     }
     __syncthreads();
   }
-  const float a = wave_sum(sse), b = wave_sum(sae);
+  const float a = wave_sum(hacc[threadIdx.x * 4 + 0]), b = wave_sum(hacc[threadIdx.x * 4 + 1]);
   if (lane == 0) { red[wave] = a; red[MLP2_MAXW + wave] = b; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -345,27 +444,29 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) mlp2_kernel(Args args) {
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
-template <int KH, int RBW, bool DROP>
-static mlp2_fn pick_act(int act) {
-  if (act == ACT_TANH) return mlp2_kernel<KH, RBW, ACT_TANH, DROP>;
-  if (act == ACT_SOFTSIGN) return mlp2_kernel<KH, RBW, ACT_SOFTSIGN, DROP>;
-  return mlp2_kernel<KH, RBW, -1, DROP>;
+template <int KH, bool DROP, int NWM>
+static mlp2_fn pick_act(int act, int act2) {
+  if (act2 != ACT_LINEAR) return mlp2_kernel<KH, -1, DROP, NWM>;
+  if (act == ACT_TANH) return mlp2_kernel<KH, ACT_TANH, DROP, NWM>;
+  if (act == ACT_SOFTSIGN) return mlp2_kernel<KH, ACT_SOFTSIGN, DROP, NWM>;
+  return mlp2_kernel<KH, -1, DROP, NWM>;
 }
 
 template <bool DROP>
-static mlp2_fn pick_d(int kh, int rbw, int act) {
-  if (rbw == 1) {
-    if (kh == 44) return pick_act<44, 1, DROP>(act);  // 88-channel BlazeFace tap (Model-88)
-    if (kh == 48) return pick_act<48, 1, DROP>(act);  // 96-channel tap (Model-96)
-  } else if (rbw == 2) {
-    if (kh == 44) return pick_act<44, 2, DROP>(act);
-    if (kh == 48) return pick_act<48, 2, DROP>(act);
+static mlp2_fn pick_d(int kh, int act, int act2, int ncb) {
+  if (ncb <= 4) {
+    if (kh == 44) return pick_act<44, DROP, 4>(act, act2);  // 88-channel BlazeFace tap (Model-88)
+    if (kh == 48) return pick_act<48, DROP, 4>(act, act2);  // 96-channel tap (Model-96)
   }
+  if (kh == 44) return pick_act<44, DROP, MLP2_MAXW>(act, act2);
+  if (kh == 48) return pick_act<48, DROP, MLP2_MAXW>(act, act2);
   return nullptr;
 }
 
-static mlp2_fn pick(int kh, int rbw, int act, int drop) {
-  return drop >= 0 ? pick_d<true>(kh, rbw, act) : pick_d<false>(kh, rbw, act);
+static mlp2_fn pick(const int* w) {
+  const int* o = w + w[H_OPS_OFF];
+  const int kh = ((o[O_K] + 7) & ~7) / 2, act = o[O_EACT], act2 = o[O_AUX2];
+  return o[O_EDROP] >= 0 ? pick_d<true>(kh, act, act2, o[O_MODE]) : pick_d<false>(kh, act, act2, o[O_MODE]);
 }
 
 static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int& act, int& drop) {
@@ -377,17 +478,16 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   kh = cp / 2;
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
-  const int T = 32 * rbw;
-  const int xst = ((cp >> 2) & 1) ? cp : cp + 4;
-  lds_bytes = (T * xst + ncb * T * 4 + T * 4 + 2 * 1024) * 4;
+  const int T = 32;
+  lds_bytes = (2 * MLP2_XF + 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64) * 4;
 }
 
 int mlp2_supported(const int* w) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
   const int* o = w + w[H_OPS_OFF];
-  return pick(kh, rbw, act, drop) != nullptr && ncb >= 1 && ncb <= MLP2_MAXW && o[O_AUX3] == 3 &&
-         (o[O_K] & 3) == 0 && lds <= 160 * 1024;
+  return pick(w) != nullptr && rbw == 1 && ncb >= 1 && ncb <= MLP2_MAXW &&
+         o[O_AUX3] == 3 && (o[O_K] & 3) == 0 && o[O_K] <= 96 && lds <= 160 * 1024;
 }
 
 int mlp2_grid_cap(const int* w, int n_cu) {
@@ -395,7 +495,7 @@ int mlp2_grid_cap(const int* w, int n_cu) {
   geom(w, kh, rbw, ncb, lds, act, drop);
   hipFuncAttributes attr;
   int per_cu = 1;
-  if (hipFuncGetAttributes(&attr, (const void*)pick(kh, rbw, act, drop)) == hipSuccess) {
+  if (hipFuncGetAttributes(&attr, (const void*)pick(w)) == hipSuccess) {
     const int vg = ((attr.numRegs + 7) / 8) * 8;
     const int waves_simd = vg > 0 ? (512 / vg > 8 ? 8 : 512 / vg) : 8;
     per_cu = (4 * waves_simd) / ncb;
@@ -409,7 +509,7 @@ int mlp2_grid_cap(const int* w, int n_cu) {
 int mlp2_launch(const int* w, const Args& a, int grid, hipStream_t s) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
-  mlp2_fn k = pick(kh, rbw, act, drop);
+  mlp2_fn k = pick(w);
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   hipLaunchKernelGGL(k, dim3(grid), dim3(ncb * 64), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;

@@ -672,13 +672,30 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
 }
 
 // grad[i] = sum_g ws[g][i]  (fixed order over workgroups)
-__global__ void reduce_kernel(const float* __restrict__ ws, float* __restrict__ grad, int grid,
-                              int slab, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int g = 0; g < grid; ++g) s += ws[(size_t)g * slab + i];
-  grad[i] = s;
+// per-workgroup gradient slabs -> flat gradient.  A workgroup owns 64 consecutive parameters;
+// wave w sums slabs w, w+4, ... with 4 independent accumulators (16 loads in flight per lane),
+// then the 4 wave partials are added in fixed order: deterministic, and ~grid/16 dependent
+// latencies instead of grid.
+__global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ ws, float* __restrict__ grad,
+                                                     int grid, int slab, int n) {
+  __shared__ float part[4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int i = blockIdx.x * 64 + l;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < n) {
+    const float* p = ws + i;
+    int g = w;
+    for (; g + 12 < grid; g += 16) {
+      s0 += p[(size_t)g * slab];
+      s1 += p[(size_t)(g + 4) * slab];
+      s2 += p[(size_t)(g + 8) * slab];
+      s3 += p[(size_t)(g + 12) * slab];
+    }
+    for (; g < grid; g += 4) s0 += p[(size_t)g * slab];
+  }
+  part[w][l] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && i < n) grad[i] = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
 }
 
 // Keras legacy optimizers (TF ApplyGradientDescent / ApplyAdam / ApplyAdaMax functors)
@@ -891,7 +908,7 @@ extern "C" int hpe_reduce(const hpe_program* p, int64_t n_rows, const void* ws, 
   if (!p || !ws || !grad) return fail(HPE_EINVAL, "hpe_reduce: null argument");
   const int grid = hpe_launch_grid(p, n_rows);
   const int n = p->hdr[H_NPARAMS_TRAIN] + 4;
-  hipLaunchKernelGGL(reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, (hipStream_t)stream,
                      (const float*)ws, grad, grid, p->hdr[H_SLAB], n);
   HIPCHK(hipGetLastError());
   return HPE_OK;
