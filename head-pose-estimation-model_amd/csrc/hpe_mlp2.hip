@@ -279,42 +279,32 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       // park A1 in LDS across the head phase (16 VGPRs fewer live through the loss epilogue)
 #pragma unroll
       for (int g = 0; g < 16; ++g) a1s[(wave * 16 + g) * 64 + lane] = acc[g];
-      // head partials: per output j, reduce-scatter the 16 row values over the 32 lanes of a
-      // half (offsets 16, 8, 4, 2 halve the vector; xor 1 completes) -> lane holds row
-      // g = (lane >> 1) & 15 of this half
-      const int gsel = (lane >> 1) & 15;
-      const int rsel = (gsel & 3) + 8 * (gsel >> 2) + 4 * half;
+      // head partials from the parked A1 (a row-on-lane read of this wave's own LDS region, no
+      // cross-lane shuffles): lane (row r = l32, half h) dots A1[r][16 h .. 16 h + 16) with the
+      // matching W2 rows, the two halves are combined with one xor-32 exchange
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      {
+        const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
+        const float* ar = a1s + (wave * 16 + gr) * 64 + hh * 32 + 16 * half;
+        const float* wr = w2t + (wave * 32 + 16 * half) * 4;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        float v[16];
-        const float w2j = w2t[n * 4 + j];
+        for (int i = 0; i < 16; i += 4) {
+          const f32x4 av = *(const f32x4*)(ar + i);
 #pragma unroll
-        for (int g = 0; g < 16; ++g) v[g] = acc[g] * w2j;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bool up = lane & 16;
-          const float snd = up ? v[i] : v[i + 8];
-          v[i] = (up ? v[i + 8] : v[i]) + __shfl_xor(snd, 16, 64);
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 w = *(const f32x4*)(wr + (i + e) * 4);
+            s0 = fmaf(av[e], w.x, s0);
+            s1 = fmaf(av[e], w.y, s1);
+            s2 = fmaf(av[e], w.z, s2);
+          }
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool up = lane & 8;
-          const float snd = up ? v[i] : v[i + 4];
-          v[i] = (up ? v[i + 4] : v[i]) + __shfl_xor(snd, 8, 64);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const bool up = lane & 4;
-          const float snd = up ? v[i] : v[i + 2];
-          v[i] = (up ? v[i + 2] : v[i]) + __shfl_xor(snd, 4, 64);
-        }
-        {
-          const bool up = lane & 2;
-          const float snd = up ? v[0] : v[1];
-          v[0] = (up ? v[1] : v[0]) + __shfl_xor(snd, 2, 64);
-        }
-        v[0] += __shfl_xor(v[0], 1, 64);
-        if ((lane & 1) == 0) part[(wave * T + rsel) * 4 + j] = v[0];
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (half == 0) *(f32x4*)(part + (wave * T + r) * 4) = f32x4{s0, s1, s2, 0.f};
       }
     }
     bar_lds();
