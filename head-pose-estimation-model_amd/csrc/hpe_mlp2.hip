@@ -60,11 +60,16 @@ struct E2 {
 // image of tile row r: tile = rows [row0, row0 + 32) with row0 = img0 * P + rem0 (no 64-bit
 // division per row; at P >= 32 a tile straddles at most one image boundary)
 struct TileImg {
-  int64_t img0;
-  int rem0, P;
-  __device__ __forceinline__ int64_t of(int r) const {
+  int img0, rem0, P;
+  __device__ __forceinline__ int of(int r) const {
     const int t = rem0 + r;
     return img0 + (P >= 32 ? (t >= P ? 1 : 0) : (P == 1 ? t : t / P));
+  }
+  // advance by S rows, (dq, dr) = divmod(S, P) precomputed
+  __device__ __forceinline__ void advance(int dq, int dr) {
+    img0 += dq;
+    rem0 += dr;
+    if (rem0 >= P) { rem0 -= P; ++img0; }
   }
 };
 
@@ -111,18 +116,32 @@ __device__ __forceinline__ float act1_g(int act, float a) {
 // batches): lane l looks up the source image of tile row l once, before any piece is issued, so
 // the only wait in here never drains an in-flight prefetch.
 __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* lab, int64_t row0,
-                                           int wave, int NCB, int lane, int Cin, bool labels) {
-  const int64_t nrows = args.nrows;
-  const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
+                                           const TileImg& ti, int wave, int NCB, int lane, int Cin,
+                                           bool labels) {
+  const int64_t rem = args.nrows - 1 - row0;
+  const int last = rem < 31 ? (int)rem : 31;
   const int P = args.P;
-  TileImg ti;
-  ti.P = P;
-  ti.img0 = row0 / P;
-  ti.rem0 = (int)(row0 - ti.img0 * P);
+  const int q = Cin >> 2;
+  if (!args.idx && P >= 32) {
+    // contiguous rows, at most two images per tile: no lookups, no cross-lane traffic
+    if (labels && wave == 0) {
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int slot = pc * 64 + lane;
+        const int r = min(slot >> 2, last), j = min(slot & 3, 2);
+        glds4(args.ytrue + (int64_t)ti.of(r) * 3 + j, lds_addr(lab + pc * 64));
+      }
+    }
+    for (int r = wave; r < 32; r += NCB) {
+      const int64_t srow = row0 + min(r, last);
+      if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
+    }
+    return;
+  }
   const int lr = min(lane & 31, last);
-  const int64_t limg = ti.of(lr);
-  const int lpos = (int)(row0 + lr - limg * P);
-  const int64_t lsrc = args.idx ? (int64_t)args.idx[limg] : limg;  // source image of tile row lr
+  const int limg = ti.of(lr);
+  const int lpos = (int)(row0 + lr - (int64_t)limg * P);
+  const int lsrc = args.idx ? args.idx[limg] : limg;  // source image of tile row lr
   // retire the index load here, visibly to hipcc's waitcnt pass (vmcnt(0)): otherwise it waits
   // for it (and so for every LDS-DMA piece issued below) at the next reuse of its register
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -131,14 +150,13 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
     for (int pc = 0; pc < 2; ++pc) {
       const int slot = pc * 64 + lane;
       const int r = min(slot >> 2, last), j = min(slot & 3, 2);
-      const int64_t src = (int64_t)__shfl((int)lsrc, r, 64);
+      const int64_t src = __shfl(lsrc, r, 64);
       glds4(args.ytrue + src * 3 + j, lds_addr(lab + pc * 64));
     }
   }
-  const int q = Cin >> 2;
   for (int r = wave; r < 32; r += NCB) {
     const int rr = min(r, last);
-    const int64_t srow = (int64_t)__builtin_amdgcn_readlane((int)lsrc, rr) * P +
+    const int64_t srow = (int64_t)__builtin_amdgcn_readlane(lsrc, rr) * P +
                          __builtin_amdgcn_readlane(lpos, rr);
     if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
   }
@@ -215,25 +233,27 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     if (c < ((Cin + 7) & ~7)) xbuf[r * MLP2_XS + c] = 0.f;
   }
   __syncthreads();
-  if (blockIdx.x < ntiles) {
-    stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, wave, NCB, lane, Cin, labels);
-  }
+  // tile -> (first image, row within it), advanced incrementally (no 64-bit division per tile)
+  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = (int)(blockIdx.x * T / P);
+  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
+  if (blockIdx.x < ntiles) stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, ti, wave, NCB, lane, Cin, labels);
   int buf = 0;
-  for (int tile = blockIdx.x; tile < (int)ntiles; tile += gridDim.x, buf ^= 1) {
+  for (int tile = blockIdx.x; tile < (int)ntiles; tile += gridDim.x, buf ^= 1, ti.advance(dq, dr)) {
     const int64_t row0 = (int64_t)tile * T;
     const float* xs = xbuf + buf * MLP2_XF;
     const float* lab = lbuf + buf * MLP2_LAB;
-    TileImg ti;
-    ti.P = P;
-    ti.img0 = row0 / P;
-    ti.rem0 = (int)(row0 - ti.img0 * P);
     // tile `tile` landed (own pieces) -> barrier: every wave's pieces landed, and every wave is
     // done with tile - gridDim.x, whose buffer the prefetch below overwrites
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar_lds();
     if (tile + gridDim.x < ntiles) {
+      TileImg tn = ti;
+      tn.advance(dq, dr);
       stage_tile(args, xbuf + (buf ^ 1) * MLP2_XF, lbuf + (buf ^ 1) * MLP2_LAB,
-                 (int64_t)(tile + gridDim.x) * T, wave, NCB, lane, Cin, labels);
+                 (int64_t)(tile + gridDim.x) * T, tn, wave, NCB, lane, Cin, labels);
     }
 
     // ---- forward: Z1 = X.W1 (+b1, act, dropout) and the head partials ----
@@ -314,7 +334,11 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       const int r = it / 3, j = it - r * 3;
       const int64_t R = row0 + r;
       float z = b2t[j];
-      for (int w = 0; w < NCB; ++w) z += part[(w * T + r) * 4 + j];
+      float pv[MLP2_MAXW];  // all partial loads in flight, summed in fixed wave order
+#pragma unroll
+      for (int w = 0; w < MLP2_MAXW; ++w) pv[w] = w < NCB ? part[(w * T + r) * 4 + j] : 0.f;
+#pragma unroll
+      for (int w = 0; w < MLP2_MAXW; ++w) z += pv[w];
       const int64_t img = ti.of(r) + args.img_off;
       // ACT1 >= 0 kernels are only picked for a linear head (the create_model family)
       const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr

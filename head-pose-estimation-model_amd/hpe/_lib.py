@@ -5,7 +5,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libhpe.so')
+LIB_PATH = os.environ.get('HPE_LIB') or os.path.join(_HERE, 'libhpe.so')  # HPE_LIB: debug builds
 
 # symbol -> (restype, argtypes), exactly the declarations of include/hpe.h
 _vp, _i32, _i64, _f, _u64, _sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
