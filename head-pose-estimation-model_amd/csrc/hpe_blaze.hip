@@ -10,7 +10,8 @@
 // Every op is one fused kernel: the input tile (+ halo) is staged HBM -> LDS once; each wave owns
 // 32 output positions and computes the depthwise result just in time, in registers, as the A
 // operand of v_mfma_f32_32x32x2_f32 (lane = position, k = channel, 4 channels per ds_read_b128 per
-// tap), so the depthwise output never exists in memory; the pointwise weights (W^T) sit in LDS and
+// tap; fp16-split MFMA, see mfma_split), so the depthwise output never exists in memory; the
+// pointwise weights (W^T, as fp16 hi/lo pairs) sit in LDS and
 // the epilogue adds bias + residual (read back from the staged tile) + ReLU and writes NHWC.
 // fp32 throughout (exact-f32 MFMA): per-op HBM traffic = input + output, the depthwise layers'
 // 1.9 FLOP/B make the chain HBM-bound.
@@ -33,6 +34,32 @@ struct BfArgs {
 };
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+
+// Pointwise convs on fp16 MFMA (configs[4]: "fp16 MFMA on pointwise convs") at fp32 accuracy:
+// a = a_hi + a_lo, b = b_hi + b_lo with fp16 halves, a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi
+// (dropped a_lo.b_lo ~ 2^-22 relative), fp32 accumulate: three v_mfma_f32_32x32x8_f16 per 8
+// channels replace four v_mfma_f32_32x32x2_f32 (64 cycles each) per 8 channels.  The W^T table
+// holds each quad of weights as {hi[4], lo[4]} (16 B, the footprint of the fp32 quad it replaces).
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ h4 to_h4(f32x4 v) {
+  return h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+}
+__device__ __forceinline__ f32x4 split_w(f32x4 v) {  // fp32 quad -> packed {hi[4], lo[4]}
+  const h4 hi = to_h4(v);
+  const h4 lo = to_h4(v - f32x4{(float)hi.x, (float)hi.y, (float)hi.z, (float)hi.w});
+  h8 r = {hi.x, hi.y, hi.z, hi.w, lo.x, lo.y, lo.z, lo.w};
+  return *(f32x4*)&r;
+}
+__device__ __forceinline__ f32x16 mfma_split(f32x4 av, f32x4 wpk, f32x16 acc) {
+  const h4 ah = to_h4(av);
+  const h4 al = to_h4(av - f32x4{(float)ah.x, (float)ah.y, (float)ah.z, (float)ah.w});
+  const h8 w = *(const h8*)&wpk;
+  const h4 bh = {w[0], w[1], w[2], w[3]}, bl = {w[4], w[5], w[6], w[7]};
+  acc = __builtin_amdgcn_mfma_f32_32x32x8f16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x8f16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x8f16(ah, bh, acc, 0, 0, 0);
+}
 
 // XCD-aware work id: consecutive work ids (the tiles of one image, whose halos overlap) stay on
 // one XCD's L2 (hardware dispatches workgroups round-robin over the 8 XCDs).
@@ -141,7 +168,7 @@ __global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
   if (tc < cstep) {
     for (int n = tc; n < NCT * 32; n += cstep) {
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (n < Coutp) v = ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * tq);
+      if (n < Coutp) v = split_w(ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * tq));
       *(f32x4*)(wt + n * KS + 4 * tq) = v;
     }
     const int iy0 = oy0 * S - padt;
@@ -199,11 +226,7 @@ __global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
       }
 #pragma unroll
       for (int nc = 0; nc < NC; ++nc) {
-        const f32x4 bv = ld4(wb + nc * 32 * KS + c0);
-        acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[nc], 0, 0, 0);
-        acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[nc], 0, 0, 0);
-        acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc[nc], 0, 0, 0);
-        acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc[nc], 0, 0, 0);
+        acc[nc] = mfma_split(av, ld4(wb + nc * 32 * KS + c0), acc[nc]);
       }
     }
     // ---- epilogue: lane = output channel n, registers = 16 positions of the chunk ----
@@ -289,7 +312,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
   for (int i = threadIdx.x; i < NCT * 32 * kq; i += nthr) {
     const int n = i / kq, q = i - n * kq;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (n < Coutp) v = ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * q);
+    if (n < Coutp) v = split_w(ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * q));
     *(f32x4*)(wt + n * KS + 4 * q) = v;
   }
   for (int i = threadIdx.x; i < 10 * kq; i += nthr) *(f32x4*)(dwt + 4 * i) = ld4(P_ + f[BFO_DWW] + 4 * i);
@@ -360,11 +383,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
         }
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
-          const f32x4 bv = ld4(wb + nc * 32 * KS + c0);
-          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc[nc], 0, 0, 0);
-          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc[nc], 0, 0, 0);
-          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc[nc], 0, 0, 0);
-          acc[nc] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc[nc], 0, 0, 0);
+          acc[nc] = mfma_split(av, ld4(wb + nc * 32 * KS + c0), acc[nc]);
         }
       }
       // epilogue: register g <-> position x0 + 4*half + (g&3) + 8*(g>>2) of row oyc
