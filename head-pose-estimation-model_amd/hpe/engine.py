@@ -101,6 +101,8 @@ class Engine:
         return out
 
     def set_weights(self, wdict):
+        if hasattr(self, '_spatial'):
+            del self._spatial  # rebuilt from the new weights on the next H x W > 1 forward
         flat = self.params[:self.n_train].detach().cpu().numpy().copy()
         for k, a in wdict.items():
             o, shp = self.layout.param_index[k]
@@ -113,8 +115,22 @@ class Engine:
         self.weights.update({k: np.asarray(v, dtype=np.float32) for k, v in wdict.items()})
 
     # -- compute ------------------------------------------------------------------------------
+    def spatial(self):
+        """Staged executor for graphs with ops that are not row-local on H x W > 1 maps (SE gate,
+        spatial MHA, terminal GAP: hpe/spatial.py), or None."""
+        if not hasattr(self, '_spatial'):
+            from .spatial import SpatialHead, is_spatial
+            self._spatial = SpatialHead(self.model_config, self.get_weights(), self.device) \
+                if is_spatial(self.model_config) else None
+        return self._spatial
+
     def forward(self, x, P, idx=None, out=None):
-        """x: device fp32 [n_images*P, C_in] (rows); returns [n_images*P, C_out]."""
+        """x: device fp32 [n_images*P, C_in] (rows); returns [n_images*P, C_out] ([n_images, C_out]
+        for a graph ending in GlobalAveragePooling2D at P > 1)."""
+        if P > 1 and self.spatial() is not None:
+            if idx is not None:
+                raise ValueError('gathered batches of attention heads on H x W > 1 maps are not supported')
+            return self._spatial.forward(x, P, out=out)
         c = self.program('fwd', P)
         n_img = x.shape[0] // P if idx is None else idx.numel()
         if out is None:
@@ -126,6 +142,9 @@ class Engine:
 
     def loss_sums(self, x, y, P, idx=None, n_images=None):
         """Eval pass: returns device tensor [sum e^2, sum |e|, ...] (grad buffer layout)."""
+        if P > 1 and self.spatial() is not None:
+            raise ValueError('evaluate / fit of attention heads runs on 1x1 maps (the reference '
+                             'trains them at P = 1, train_88.py:270-305); use predict on H x W maps')
         c = self.program('eval', P)
         n_img = n_images if n_images is not None else (x.shape[0] // P if idx is None else idx.numel())
         lib = _lib.load()
@@ -139,6 +158,8 @@ class Engine:
 
     def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0):
         """fwd + loss + bwd over this rank's images; self.grad = [dL/dparams..., sse, sae, 0, 0]."""
+        if P > 1 and self.spatial() is not None:
+            raise ValueError('fit of attention heads runs on 1x1 maps (train_88.py:270-305)')
         c = self.program('train', P)
         lib = _lib.load()
         ws = c.workspace(n_images * P, self.device)

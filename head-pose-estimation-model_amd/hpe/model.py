@@ -176,9 +176,15 @@ class Model:
         outputs = self._config['output_layers']
         # spatial output unless the graph flattens (Flatten / Dense head on (C,))
         spatial = True
+        names = {l['name']: l for l in self._config['layers']}
         for l in self._config['layers']:
             if l['class_name'] in ('Flatten',):
                 spatial = False
+            if l['class_name'] == 'GlobalAveragePooling2D':
+                # a pooled output (create_model -> GAP), not the SE squeeze of the model input
+                src = [t[0] for node in l.get('inbound_nodes') or [] for t in node]
+                if not all(names.get(s, {}).get('class_name') == 'InputLayer' for s in src):
+                    spatial = False
         if len(xshape) == 4 and spatial:
             return (n, xshape[1], xshape[2], 3)
         return (n, 3)

@@ -132,6 +132,23 @@ int hpe_detect(const float *cls0, const float *cls1, const float *loc0, const fl
 
 const char *hpe_last_error(void);
 
+/* Attention heads on H x W > 1 feature maps: the two stages that are not
+ * row-local.  Replace the TF kernels behind GlobalAveragePooling2D -> Dense -> Dense -> Multiply
+ * (Model-88/attention_model.py:34-38, :78-82) and behind MultiHeadAttention's softmax(QK^T)V over
+ * the H*W tokens of each image (attention_model.py:52-55).
+ *
+ * hpe_se_gate: x, xg [n_images * P][C] rows; w1 [C][U] (+ b1 [U], may be NULL), w2 [U][C]
+ * (+ b2 [C]); act1 / act2 activation codes of csrc/hpe_prog.h (ACT_*).  xg = x * s[image].
+ * hpe_mha: per row, in = [pass-through C | q H*D (pre-scaled by 1/sqrt(D)) | k H*D | v H*D]
+ * (stride ld_in floats); out = [pass-through C | o H*D] (stride ld_out).  1 <= D <= 64. */
+int hpe_se_gate(const float *x, float *xg, int64_t n_images, int32_t P, int32_t C, const float *w1,
+                const float *b1, int32_t U, int32_t act1, const float *w2, const float *b2,
+                int32_t act2, void *stream);
+/* y[i][c] = mean over the P rows of image i of x (a terminal GlobalAveragePooling2D), C <= 256. */
+int hpe_seg_mean(const float *x, float *y, int64_t n_images, int32_t P, int32_t C, void *stream);
+int hpe_mha(const float *in, int32_t ld_in, int32_t C, float *out, int32_t ld_out,
+            int64_t n_images, int32_t P, int32_t H, int32_t D, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,149 @@
+"""Attention heads on H x W > 1 maps (SURVEY.md §8 a9 SE, a10 spatial MHA; hpe/spatial.py).
+
+CPU: the staged decomposition (SE gate -> program B -> attention core -> program D) emulated in
+numpy (the row programs by the row-program emulator) against the oracle's forward of the
+reference graph on 16x16 / 8x8 maps, for every SE + MHA checkpoint signature and for the
+create_modelC (SE only) builder.  GPU: the HIP path (hpe_se_gate, hpe_mha, row programs) against
+the oracle.  Parity source: oracle/keras_ref.py restates Keras GAP / MultiHeadAttention /
+LayerNormalization (attention_model.py:34-72); no TF output exists for H x W > 1 (parity unpinned
+beyond the restatement).
+"""
+import numpy as np
+import pytest
+
+import hpe.compiler as C
+from hpe.spatial import SpatialPlan, is_spatial
+import rowprog_emu as EMU
+from oracle import keras_ref as K
+from util import fixture, index
+
+SPATIAL_IDS = [r for r in sorted(index()) if not r.startswith('reg1') and is_spatial(fixture(r)[0])]
+
+
+def _flat(prog, w):
+    p = np.zeros(prog.n_params)
+    for k, (o, shp) in prog.param_index.items():
+        p[o:o + int(np.prod(shp))] = w[k].ravel()
+    p[prog.n_train:] = prog.consts
+    return p
+
+
+def _act(a, z):
+    return EMU._act(a, z)
+
+
+def _emulate(plan, x, P):
+    """numpy restatement of the four stages (float64)."""
+    n = x.shape[0] // P
+    xg = x.astype(np.float64)
+    if plan.pool:
+        pd = C.compile_graph(plan.head_config, plan.head_weights, 'fwd', fused=False)
+        rows = EMU.run(pd, _flat(pd, plan.head_weights), xg)['out']
+        return rows.reshape(n, P, -1).mean(axis=1)
+    if plan.se is not None:
+        s = plan.se
+        m = xg.reshape(n, P, -1).mean(axis=1)
+        h = _act(s['act1'], m @ s['w1'] + s['b1'])
+        g = _act(s['act2'], h @ s['w2'] + s['b2'])
+        xg = (xg.reshape(n, P, -1) * g[:, None, :]).reshape(n * P, -1)
+    if plan.mha is None:
+        pd = C.compile_graph(plan.head_config, plan.head_weights, 'fwd', fused=False)
+        return EMU.run(pd, _flat(pd, plan.head_weights), xg)['out']
+    H, D = plan.mha['H'], plan.mha['D']
+    pb = C.compile_graph(plan.qkv_config, plan.qkv_weights, 'fwd', fused=False)
+    qkv = EMU.run(pb, _flat(pb, plan.qkv_weights), xg)['out']
+    Cc = plan.C
+    q = qkv[:, Cc:Cc + H * D].reshape(n, P, H, D)
+    k = qkv[:, Cc + H * D:Cc + 2 * H * D].reshape(n, P, H, D)
+    v = qkv[:, Cc + 2 * H * D:].reshape(n, P, H, D)
+    s = np.einsum('bthd,bshd->bhts', q, k)
+    a = np.exp(s - s.max(-1, keepdims=True))
+    a /= a.sum(-1, keepdims=True)
+    o = np.einsum('bhts,bshd->bthd', a, v).reshape(n * P, H * D)
+    pd = C.compile_graph(plan.head_config, plan.head_weights, 'fwd', fused=False)
+    return EMU.run(pd, _flat(pd, plan.head_weights), np.concatenate([qkv[:, :Cc], o], axis=1))['out']
+
+
+def _modelC():
+    """attention_model.py:74-90 create_modelC (SE r=8 -> 11 units, 1x1-conv head), seeded weights."""
+    from hpe import keras
+    keras.backend.clear_session()
+    inp = keras.Input((None, None, 88))
+    se = keras.layers.GlobalAveragePooling2D()(inp)
+    se = keras.layers.Dense(11, activation='relu')(se)
+    se = keras.layers.Dense(88, activation='sigmoid')(se)
+    se = keras.layers.Reshape((1, 1, 88))(se)
+    x = keras.layers.Multiply()([inp, se])
+    x = keras.layers.Conv2D(42, 1, activation='relu')(x)
+    out = keras.layers.Conv2D(3, 1, activation=None)(x)
+    m = keras.Model(inp, out)
+    return m.model_config, m.weights_dict()
+
+
+def _inputs(n, h, w, c, seed):
+    rng = np.random.default_rng(seed)
+    return np.maximum(0.0, 0.6 * rng.standard_normal((n, h, w, c)) - 0.3).astype(np.float32)
+
+
+def test_spatial_fixtures_present():
+    assert len(SPATIAL_IDS) >= 5
+
+
+@pytest.mark.parametrize('hw', [(16, 16), (8, 8)])
+@pytest.mark.parametrize('rid', SPATIAL_IDS + ['create_modelC'])
+def test_staged_decomposition_matches_oracle(rid, hw):
+    mc, w = _modelC() if rid == 'create_modelC' else fixture(rid)
+    c = mc['config']['layers'][0]['config']['batch_input_shape'][-1]
+    x = _inputs(3, hw[0], hw[1], c, seed=sum(map(ord, rid)))
+    ref = K.Graph(mc, w).forward(x).detach().numpy().reshape(-1, 3)
+    plan = SpatialPlan(mc, w)
+    got = _emulate(plan, x.reshape(-1, c), hw[0] * hw[1]).reshape(-1, 3)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_row_local_graph_is_not_spatial():
+    mc, w = fixture('hrchr82r')
+    assert not is_spatial(mc)
+    with pytest.raises(ValueError):
+        SpatialPlan(mc, w)
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU: the HIP path
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize('hw', [(16, 16), (8, 8), (5, 7)])
+@pytest.mark.parametrize('rid', SPATIAL_IDS + ['create_modelC'])
+def test_gpu_spatial_predict_matches_oracle(rid, hw):
+    import hpe
+    mc, w = _modelC() if rid == 'create_modelC' else fixture(rid)
+    c = mc['config']['layers'][0]['config']['batch_input_shape'][-1]
+    x = _inputs(5, hw[0], hw[1], c, seed=7)
+    ref = K.Graph(mc, w).forward(x).detach().numpy()
+    m = hpe.model_from_config(mc, w)
+    got = m.predict(x)
+    assert got.shape == ref.shape
+    # fp32 throughout; softmax over up to 256 tokens in fp32 (tolerance stated here)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_spatial_large_map_and_p1_consistency():
+    """48x48 maps (P = 2304 tokens: the attention streams 9 key blocks through LDS) on two images,
+    and the P = 1 layout through the staged path equals the row program's."""
+    import torch
+    import hpe
+    from hpe.spatial import SpatialHead
+    rid = SPATIAL_IDS[0]
+    mc, w = fixture(rid)
+    c = mc['config']['layers'][0]['config']['batch_input_shape'][-1]
+    x = _inputs(2, 48, 48, c, seed=3)
+    ref = K.Graph(mc, w).forward(x).detach().numpy()
+    got = hpe.model_from_config(mc, w).predict(x)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=5e-4)
+    x1 = _inputs(64, 1, 1, c, seed=4)
+    m = hpe.model_from_config(mc, w)
+    row = m.predict(x1).reshape(-1, 3)
+    sh = SpatialHead(mc, w, torch.device('cuda'))
+    staged = sh.forward(torch.from_numpy(x1.reshape(-1, c)).cuda(), 1).cpu().numpy()
+    np.testing.assert_allclose(staged, row, rtol=1e-5, atol=1e-5)
