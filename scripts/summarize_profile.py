@@ -51,11 +51,11 @@ def main(tag):
         fb, wb, _ = per[short]
         res[key] = {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb, 'hbm_bytes_per_launch': fb + wb}
 
-    # bench lines -> their dominant kernels (template args: <KH, RBW, ACT1, DROP>; ACT 1 = tanh, 3 = softsign)
+    # bench lines -> their dominant kernels (template args: <KH, ACT1, DROP, NWM>; ACT 1 = tanh, 3 = softsign)
     for short in per:
-        if short.startswith('void mlp2_kernel<48') and short.endswith('false>'):
+        if short.startswith('void mlp2_kernel<48') and ', false' in short:
             put('train', short)
-        elif short.startswith('void mlp2_kernel<44') and short.endswith('true>'):
+        elif short.startswith('void mlp2_kernel<44') and ', true' in short:
             put('train88', short)
         elif 'chain_fwd' in short:
             put('infer', short)
