@@ -96,13 +96,23 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
   // column padl (zeros around), no per-element division
   const int iy0 = oy0 * 2 - f[BFO_PADT];
   const int padl3 = f[BFO_PADL] * 3, rowf = COLS * 3, W3 = W * 3;
-  for (int r = 0; r < ROWS; ++r) {
-    const int iy = iy0 + r;
-    const bool rin = iy >= 0 && iy < H && img < a.nimg;
-    const float* srow = a.src + ((img * H + (rin ? iy : 0)) * W) * 3;
-    for (int e = threadIdx.x; e < rowf; e += blockDim.x) {
-      const int x3 = e - padl3;
-      lds[r * rowf + e] = (rin && x3 >= 0 && x3 < W3) ? srow[x3] : 0.f;
+  // batches of 8 loads per thread, all issued (from clamped addresses) before the LDS writes
+  const int nT = ROWS * rowf;
+  for (int e0 = threadIdx.x; e0 < nT; e0 += 8 * blockDim.x) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = e0 + i * blockDim.x;
+      const int r = e / rowf, x3 = e - r * rowf - padl3;
+      const int iy = iy0 + r;
+      const bool ok = e < nT && iy >= 0 && iy < H && x3 >= 0 && x3 < W3 && img < a.nimg;
+      v[i] = a.src[ok ? (img * H + iy) * W * 3 + x3 : 0];
+      if (!ok) v[i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = e0 + i * blockDim.x;
+      if (e < nT) lds[e] = v[i];
     }
   }
   __syncthreads();
@@ -161,30 +171,51 @@ __global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
   const int oy0 = NI > 1 ? 0 : (wid - (int)img0 * tpi) * TH;
 
   // ---- stage W^T (rows >= Coutp zero), depthwise table, input tile (zero outside the image) ----
-  // thread -> (quad q, first column c0), column step cstep: one division per thread, none in loops
+  // batches of 8 float4 per thread: every load of a batch is issued (from a clamped, always valid
+  // address) before the first LDS write, so a workgroup's staging costs ~one HBM round trip per
+  // batch instead of one per element (a conditional load per element serialises on vmcnt(0))
   const int kq = Cinp >> 2;
   const int nthr = blockDim.x;
-  const int tq = threadIdx.x % kq, tc = threadIdx.x / kq, cstep = nthr / kq;
-  if (tc < cstep) {
-    for (int n = tc; n < NCT * 32; n += cstep) {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (n < Coutp) v = split_w(ld4(P_ + f[BFO_PWW] + n * Cinp + 4 * tq));
-      *(f32x4*)(wt + n * KS + 4 * tq) = v;
+  {
+    const int nW = NCT * 32 * kq;
+    for (int e0 = threadIdx.x; e0 < nW; e0 += 8 * nthr) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int n = e / kq, q = e - n * kq;
+        const bool ok = e < nW && n < Coutp;
+        v[i] = ld4(P_ + f[BFO_PWW] + (ok ? n * Cinp + 4 * q : 0));
+        if (!ok) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int n = e / kq, q = e - n * kq;
+        if (e < nW) *(f32x4*)(wt + n * KS + 4 * q) = split_w(v[i]);
+      }
     }
     const int iy0 = oy0 * S - padt;
-    for (int il = 0; il < NI; ++il) {
-      const int64_t img = img0 + il;
-      for (int r = 0; r < ROWS; ++r) {
-        const int iy = iy0 + r;
-        const bool rin = iy >= 0 && iy < H && img < a.nimg;
-        const float* srow = a.src + ((img * H + (rin ? iy : 0)) * W) * Cinp + 4 * tq;
-        float* lrow = tile + ((il * ROWS + r) * COLS) * CS + 4 * tq;
-        for (int c = tc; c < COLS; c += cstep) {
-          const int ix = c - padl;
-          f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          if (rin && ix >= 0 && ix < W) v = ld4(srow + ix * Cinp);
-          *(f32x4*)(lrow + c * CS) = v;
-        }
+    const int nT = NI * ROWS * COLS * kq;
+    for (int e0 = threadIdx.x; e0 < nT; e0 += 8 * nthr) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int pix = e / kq, q = e - pix * kq;
+        const int rr = pix / COLS, c = pix - rr * COLS;
+        const int il = rr / ROWS, r = rr - il * ROWS;
+        const int64_t img = img0 + il;
+        const int iy = iy0 + r, ix = c - padl;
+        const bool ok = e < nT && iy >= 0 && iy < H && ix >= 0 && ix < W && img < a.nimg;
+        v[i] = ld4(a.src + (ok ? ((img * H + iy) * W + ix) * Cinp + 4 * q : 0));
+        if (!ok) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int pix = e / kq, q = e - pix * kq;
+        if (e < nT) *(f32x4*)(tile + pix * CS + 4 * q) = v[i];
       }
     }
   }
