@@ -504,6 +504,132 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// direct: the fused block for the small maps (16x16, 8x8) and the detector heads.  Persistent
+// workgroups keep W^T (fp16 hi/lo pairs) and the depthwise table in LDS for the whole launch; each
+// wave task is a 32-position chunk of one image with ALL output-channel chunks (no depthwise
+// recompute), its nine 3x3 taps read straight from global memory (the 9x reuse is served by
+// L1 / L2, no tile staging, no workgroup barrier in the loop), residual from global, NHWC store.
+// ------------------------------------------------------------------------------------------------
+template <int S, int DW, int NC>
+__global__ void __launch_bounds__(256) bf_direct_kernel(BfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int* f = a.f;
+  const int H = f[BFO_H], W = f[BFO_W], Wo = f[BFO_WO], Ho = f[BFO_HO];
+  const int Cinp = f[BFO_CINP], Cout = f[BFO_COUT], Coutp = f[BFO_COUTP];
+  const int KS = f[BFO_KS], padt = f[BFO_PADT], padl = f[BFO_PADL];
+  const int res = f[BFO_RES], relu = f[BFO_RELU], split = f[BFO_SPLIT], ostride = f[BFO_OSTRIDE];
+  const int NCT = f[BFO_NCT];
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lgWo = __builtin_ctz(Wo);
+  const float* P_ = a.params;
+  float* wt = lds;
+  float* dwt = wt + NCT * 32 * KS;
+  const int kq = Cinp >> 2;
+  const int nthr = blockDim.x;
+  {  // W^T (split) + depthwise table, batched loads
+    const int nW = NCT * 32 * kq;
+    for (int e0 = threadIdx.x; e0 < nW; e0 += 8 * nthr) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int n = e / kq, q = e - n * kq;
+        const bool ok = e < nW && n < Coutp;
+        v[i] = ld4(P_ + f[BFO_PWW] + (ok ? n * Cinp + 4 * q : 0));
+        if (!ok) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = e0 + i * nthr;
+        const int n = e / kq, q = e - n * kq;
+        if (e < nW) *(f32x4*)(wt + n * KS + 4 * q) = split_w(v[i]);
+      }
+    }
+    if (DW)
+      for (int i = threadIdx.x; i < 10 * kq; i += nthr) *(f32x4*)(dwt + 4 * i) = ld4(P_ + f[BFO_DWW] + 4 * i);
+  }
+  __syncthreads();
+
+  const int cpi = (Ho * Wo) >> 5;
+  const int64_t ntask = a.nimg * cpi;
+  const int nwaves = nthr >> 6;
+  const int64_t istride = (int64_t)H * W * Cinp;
+  for (int64_t task = (int64_t)blockIdx.x * nwaves + wave; task < ntask; task += (int64_t)gridDim.x * nwaves) {
+    const int64_t img = task / cpi;
+    const int chunk = (int)(task - img * cpi);
+    const float* xi = a.src + img * istride;
+    const int p = chunk * 32 + l32;
+    const int oy = p >> lgWo, ox = p & (Wo - 1);
+    int toff[9];
+    uint32_t tmask = 0;
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int iy = oy * S - padt + tp / 3, ix = ox * S - padl + tp % 3;
+      const bool ok = DW ? (iy >= 0 && iy < H && ix >= 0 && ix < W) : tp == 4;
+      toff[tp] = ok ? (iy * W + ix) * Cinp : 0;
+      tmask |= ok ? (1u << tp) : 0u;
+    }
+    if (!DW) toff[4] = (oy * W + ox) * Cinp;
+    f32x16 acc[NC];
+#pragma unroll
+    for (int nc = 0; nc < NC; ++nc) acc[nc] = (f32x16){};
+#pragma unroll 2
+    for (int c0 = 4 * half; c0 < Cinp; c0 += 8) {
+      f32x4 av;
+      if (DW) {
+        f32x4 xv[9];
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(xi + toff[tp] + c0);
+        av = ld4(dwt + 9 * Cinp + c0);
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const f32x4 x = (tmask >> tp) & 1u ? xv[tp] : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 wv = ld4(dwt + tp * Cinp + c0);
+          av.x = fmaf(x.x, wv.x, av.x);
+          av.y = fmaf(x.y, wv.y, av.y);
+          av.z = fmaf(x.z, wv.z, av.z);
+          av.w = fmaf(x.w, wv.w, av.w);
+        }
+      } else {
+        av = ld4(xi + toff[4] + c0);
+      }
+#pragma unroll
+      for (int nc = 0; nc < NC; ++nc) acc[nc] = mfma_split(av, ld4(wt + (nc * 32 + l32) * KS + c0), acc[nc]);
+    }
+    // ---- epilogue: lane = output channel n, registers = 16 positions of the chunk ----
+#pragma unroll
+    for (int nc = 0; nc < NC; ++nc) {
+      const int n = nc * 32 + l32;
+      if (n >= Coutp) continue;
+      const float bias = P_[f[BFO_PWB] + n];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        const int qy = q >> lgWo, qx = q & (Wo - 1);
+        float v = acc[nc][g] + bias;
+        if (res == BF_RES_ID) {
+          if (n < Cinp) v += xi[(qy * W + qx) * Cinp + n];
+        } else if (res == BF_RES_MAXPOOL) {
+          if (n < Cinp) {
+            const float* t = xi + ((2 * qy) * W + 2 * qx) * Cinp + n;
+            v += fmaxf(fmaxf(t[0], t[Cinp]), fmaxf(t[W * Cinp], t[W * Cinp + Cinp]));
+          }
+        }
+        if (relu) v = v > 0.f ? v : 0.f;
+        const int64_t pos = (img * Ho + qy) * Wo + qx;
+        if (split) {
+          if (n < split) a.dst[pos * split + n] = v;
+          else if (n < Cout) a.dst2[pos * (Cout - split) + (n - split)] = v;
+        } else if (n < ostride) {
+          a.dst[pos * ostride + n] = v;
+        }
+      }
+    }
+  }
+}
+
 typedef void (*bf_fn)(BfArgs);
 
 // compile-time channel specialisations of the BlazeFace 64x64 / 32x32 stages (CS = KS = CINP + 4,
@@ -545,16 +671,56 @@ static bf_fn pick_block(int s, int dw, int nc) {
   return nullptr;
 }
 
+static bf_fn pick_direct(int s, int dw, int nc) {
+#define BF_DNC(S_, DW_)                                  \
+  switch (nc) {                                          \
+    case 1: return bf_direct_kernel<S_, DW_, 1>;         \
+    case 2: return bf_direct_kernel<S_, DW_, 2>;         \
+    case 3: return bf_direct_kernel<S_, DW_, 3>;         \
+    case 4: return bf_direct_kernel<S_, DW_, 4>;         \
+    default: return nullptr;                             \
+  }
+  if (s == 1 && dw) { BF_DNC(1, 1) }
+  if (s == 2 && dw) { BF_DNC(2, 1) }
+  if (s == 1 && !dw) { BF_DNC(1, 0) }
+#undef BF_DNC
+  return nullptr;
+}
+
 struct hpe_blazeface {
   int* words;
   int n_words;
   int nops;
   int64_t act_floats;
+  int n_cu;
 };
 
 static int check_op(const int* f, int i) {
   const int kind = f[BFO_KIND];
-  if (kind != BF_STEM && kind != BF_BLOCK && kind != BF_ROWS) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
+  if (kind != BF_STEM && kind != BF_BLOCK && kind != BF_ROWS && kind != BF_DIRECT) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
+  if (kind == BF_DIRECT) {
+    const int s = f[BFO_STRIDE], dw = f[BFO_DW], wo = f[BFO_WO], ho = f[BFO_HO];
+    if (!pick_direct(s, dw, f[BFO_NC]) || f[BFO_NC] != f[BFO_NCT]) return hpe_fail(HPE_EINVAL, "blazeface op %d: no direct kernel S=%d DW=%d NC=%d", i, s, dw, f[BFO_NC]);
+    if (wo <= 0 || (wo & (wo - 1)) || (ho * wo) % 32) return hpe_fail(HPE_EINVAL, "blazeface op %d: direct kernel needs Wo a power of two, Ho*Wo % 32 == 0", i);
+    if (f[BFO_WAVES] < 1 || f[BFO_WAVES] > 4) return hpe_fail(HPE_EINVAL, "blazeface op %d: waves", i);
+    if (f[BFO_CINP] % 8 || f[BFO_CINP] < f[BFO_CIN] || f[BFO_COUTP] % 8 || f[BFO_COUTP] < f[BFO_COUT] ||
+        f[BFO_KS] < f[BFO_CINP] || f[BFO_KS] % 4 || f[BFO_NCT] < 1 || f[BFO_NCT] * 32 < f[BFO_COUTP])
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: channel geometry", i);
+    if (dw ? (s == 1 ? (f[BFO_H] != ho || f[BFO_W] != wo || f[BFO_PADT] != 1 || f[BFO_PADL] != 1)
+                     : (f[BFO_H] != 2 * ho || f[BFO_W] != 2 * wo || f[BFO_PADT] || f[BFO_PADL]))
+           : (f[BFO_H] != ho || f[BFO_W] != wo || s != 1))
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: direct kernel map geometry", i);
+    if ((f[BFO_RES] == BF_RES_MAXPOOL && s != 2) || (f[BFO_RES] == BF_RES_ID && s != 1))
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: residual / stride", i);
+    const long need = 4L * (f[BFO_NCT] * 32 * f[BFO_KS] + (dw ? 10 * f[BFO_CINP] : 0));
+    if (f[BFO_LDS] < need || f[BFO_LDS] > 160 * 1024) return hpe_fail(HPE_EINVAL, "blazeface op %d: LDS", i);
+    if (f[BFO_SRC] < 0 || f[BFO_SRC] >= BF_NBUF || f[BFO_DST] < 0 || f[BFO_DST] >= BF_NBUF) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad buffer", i);
+    if (!f[BFO_SPLIT] && (f[BFO_OSTRIDE] < f[BFO_COUT] || f[BFO_OSTRIDE] > f[BFO_COUTP]))
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: output stride", i);
+    if (f[BFO_SPLIT] && (f[BFO_DST2] < 0 || f[BFO_DST2] >= BF_NBUF || f[BFO_SPLIT] >= f[BFO_COUT]))
+      return hpe_fail(HPE_EINVAL, "blazeface op %d: bad split", i);
+    return 0;
+  }
   if (kind == BF_ROWS) {
     const int S = f[BFO_STRIDE], R = f[BFO_TH], nseg = f[BFO_NI], kq = f[BFO_CINP] / 4;
     if (!pick_rows_op(f) || !f[BFO_DW] || f[BFO_SPLIT] || !f[BFO_RELU]) return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel variant", i);
@@ -630,6 +796,10 @@ extern "C" int hpe_blazeface_create(const int32_t* words, int64_t n_words, hpe_b
   h->n_words = (int)n_words;
   h->nops = nops;
   h->act_floats = words[BFH_ACT_FLOATS];
+  int dev = 0, ncu = 256;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  h->n_cu = ncu > 0 ? ncu : 256;
   *out = h;
   return HPE_OK;
 }
@@ -670,14 +840,25 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
     a.dst = bufs[f[BFO_DST]];
     a.dst2 = f[BFO_SPLIT] ? bufs[f[BFO_DST2]] : nullptr;
     a.nimg = n_images;
-    const int64_t tpi = f[BFO_HO] / f[BFO_TH];
-    const int64_t nwg = f[BFO_KIND] == BF_ROWS ? n_images * f[BFO_NI]
-                        : f[BFO_NI] > 1 ? (n_images + f[BFO_NI] - 1) / f[BFO_NI] : n_images * tpi;
+    const int64_t tpi = f[BFO_TH] > 0 ? f[BFO_HO] / f[BFO_TH] : 1;
+    int64_t nwg;
+    if (f[BFO_KIND] == BF_DIRECT) {  // persistent: as many workgroups as fit, capped by the tasks
+      const int64_t tasks = n_images * ((f[BFO_HO] * f[BFO_WO]) >> 5);
+      int per_cu = (160 * 1024) / f[BFO_LDS];
+      if (per_cu > 12 / f[BFO_WAVES]) per_cu = 12 / f[BFO_WAVES];
+      if (per_cu < 1) per_cu = 1;
+      nwg = (tasks + f[BFO_WAVES] - 1) / f[BFO_WAVES];
+      if (nwg > (int64_t)h->n_cu * per_cu) nwg = (int64_t)h->n_cu * per_cu;
+    } else {
+      nwg = f[BFO_KIND] == BF_ROWS ? n_images * f[BFO_NI]
+            : f[BFO_NI] > 1 ? (n_images + f[BFO_NI] - 1) / f[BFO_NI] : n_images * tpi;
+    }
     if (nwg > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
     a.nwg = (int)nwg;
     const int threads = 64 * f[BFO_WAVES];
     bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel
               : f[BFO_KIND] == BF_ROWS ? pick_rows_op(f)
+              : f[BFO_KIND] == BF_DIRECT ? pick_direct(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC])
                                        : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(threads), f[BFO_LDS], s, a);

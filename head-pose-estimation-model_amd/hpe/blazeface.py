@@ -24,7 +24,20 @@ from . import _lib
 BF_MAGIC = 0x46425048
 BFH_WORDS = 8
 (BFH_MAGIC, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF) = range(4)
-BF_STEM, BF_BLOCK, BF_ROWS = 1, 2, 3
+BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT = 1, 2, 3, 4
+# 8x8 maps and the detector heads: persistent direct-tap kernel (HPE_BF_DIRECT=0 -> tiles); the
+# 16x16 maps measured equal either way and keep the tile kernel
+import os as _os
+USE_DIRECT = _os.environ.get('HPE_BF_DIRECT', '1') != '0'
+DIRECT_MAX_WO = int(_os.environ.get('HPE_BF_DIRECT_MAX_WO', '8'))
+
+
+def _direct(f, dw, cinp, nct, ks):
+    """Words of the persistent direct-tap kernel (csrc/hpe_blaze.hip bf_direct_kernel)."""
+    f[BFO_KIND] = BF_DIRECT
+    f[BFO_TH], f[BFO_NI], f[BFO_ROWS], f[BFO_COLS] = f[BFO_HO], 1, 0, 0
+    f[BFO_CS], f[BFO_KS], f[BFO_NC], f[BFO_NCT], f[BFO_WAVES] = ks, ks, nct, nct, 4
+    f[BFO_LDS] = 4 * (nct * 32 * ks + (10 * cinp if dw else 0))
 ROWS_PF = 4                 # float4 per thread the rows kernel prefetches per step (csrc RPF)
 RES_NONE, RES_ID, RES_MAXPOOL = 0, 1, 2
 BUF_IMG, BUF_A, BUF_B, BUF_OUT0 = 0, 1, 2, 3
@@ -346,6 +359,8 @@ def build_plan(model_config, weights):
         f[BFO_TH], f[BFO_NI], f[BFO_DWW], f[BFO_PWW], f[BFO_PWB] = th, ni, dww, pww, pwb
         f[BFO_CS], f[BFO_KS], f[BFO_ROWS], f[BFO_COLS], f[BFO_NC], f[BFO_LDS] = cs, ks, rows, cols, nc, lds
         f[BFO_OSTRIDE], f[BFO_NCT], f[BFO_WAVES] = coutp, nct, waves
+        if not rows_plan and USE_DIRECT and nct <= 4 and bl["Wo"] <= DIRECT_MAX_WO:
+            _direct(f, True, cinp, nct, ks)
         ops.append(f)
         if dst in (BUF_A, BUF_B):
             act_floats = max(act_floats, bl['Ho'] * bl['Wo'] * coutp)
@@ -391,6 +406,8 @@ def build_plan(model_config, weights):
         f[BFO_TH], f[BFO_NI], f[BFO_PWW], f[BFO_PWB] = th, ni, pww, pwb
         f[BFO_CS], f[BFO_KS], f[BFO_ROWS], f[BFO_COLS], f[BFO_NC], f[BFO_LDS] = cs, ks, rows, cols, nc, lds
         f[BFO_NCT], f[BFO_WAVES] = nct, waves
+        if USE_DIRECT:
+            _direct(f, False, cinp, nct, ks)
         ops.append(f)
     hdr = [0] * BFH_WORDS
     hdr[BFH_MAGIC], hdr[BFH_NOPS], hdr[BFH_ACT_FLOATS], hdr[BFH_OPS_OFF] = BF_MAGIC, len(ops), act_floats, BFH_WORDS
