@@ -128,6 +128,7 @@ class Model:
         if self._engine is None:
             from .engine import Engine
             self._engine = Engine(self.model_config, self._weights)
+            self._apply_pending_opt(self._engine)
         return self._engine
 
     def compile(self, optimizer='rmsprop', loss=None, metrics=None, **kw):
@@ -301,29 +302,125 @@ class Model:
         return hist
 
     # -- persistence --------------------------------------------------------------------------
-    def save(self, filepath, **kw):
-        """Keras-compatible content (model_config JSON + weights + legacy optimizer state) in an
-        npz container (HDF5 writer: DESIGN.md §Next)."""
+    def _h5_layer_weights(self):
+        """[(layer_name, [(keras weight name, array)])] in model.layers order, as Keras's
+        save_weights_to_hdf5_group lays them out (a nested Functional layer's variables keep their
+        own names: 'conv2d/kernel:0' under group 'model')."""
+        keys = self.weight_keys()
+        out = []
+        for l in self._config['layers']:
+            ln = l['name']
+            ws = []
+            for k in keys:
+                if not k.startswith(ln + '/'):
+                    continue
+                wn = k[len(ln) + 1:] if l['class_name'] == 'Functional' else k
+                ws.append((wn + ':0', self._weights[k]))
+            out.append((ln, ws))
+        return out
+
+    def _training_config(self):
+        if self.optimizer is None:
+            return None
+        o = self.optimizer
+        f32 = lambda v: float(np.float32(v))  # noqa: E731  (Keras stores the variables' float32 values)
+        cfg = {'name': o.name, 'learning_rate': f32(o.learning_rate), 'decay': 0.0}
+        if o.kind == 'sgd':
+            cfg.update(momentum=0.0, nesterov=False)
+        else:
+            cfg.update(beta_1=f32(o.beta_1), beta_2=f32(o.beta_2), epsilon=o.epsilon)
+            if o.kind == 'adam':
+                cfg['amsgrad'] = False
+        return {'loss': 'mse',
+                'metrics': [[{'class_name': 'MeanMetricWrapper',
+                              'config': {'name': 'mae', 'dtype': 'float32', 'fn': 'mean_absolute_error'}}]]
+                if self.compiled_metrics else None,
+                'weighted_metrics': None, 'loss_weights': None,
+                'optimizer_config': {'class_name': type(o).__name__, 'config': cfg}}
+
+    def _optimizer_state(self):
+        """Legacy Keras optimizer variables [(name, array)]: '<Opt>/iter:0', then every
+        trainable weight's m, then every v (Model-96/Trained-Models-96/*.h5 'optimizer_weights')."""
+        if self.optimizer is None:
+            return None
+        nm = type(self.optimizer).__name__
+        eng = self._engine
+        it = int(eng.iterations) if eng is not None else int(getattr(self, '_pending_opt', {}).get('iter', 0))
+        out = [('%s/iter:0' % nm, np.asarray(it, np.int64))]
+        if self.optimizer.kind == 'sgd':
+            return out
+        if eng is not None and eng.m is not None:
+            m, v = eng.m.cpu().numpy(), eng.v.cpu().numpy()
+            idx = eng.layout.param_index
+            keys = [k for k in self.weight_keys() if k in idx]
+            get = lambda a, k: a[idx[k][0]:idx[k][0] + int(np.prod(idx[k][1]))].reshape(idx[k][1])  # noqa: E731
+        else:
+            pend = getattr(self, '_pending_opt', None)
+            if not pend or not pend.get('m'):
+                return out
+            keys = [k for k in self.weight_keys() if k in pend['m']]
+            m, v = pend['m'], pend['v']
+            get = lambda a, k: a[k]  # noqa: E731
+        out += [('%s/%s/m:0' % (nm, k), get(m, k)) for k in keys]
+        out += [('%s/%s/v:0' % (nm, k), get(v, k)) for k in keys]
+        return out
+
+    def save(self, filepath, include_optimizer=True, **kw):
+        """``.h5`` / ``.hdf5``: a Keras 2.13 legacy HDF5 checkpoint (hpe.h5io.write_keras_h5), the
+        format ModelCheckpoint writes at Model-96/train_96.py:153-158 and Model-88/train_88.py:335;
+        any other name: the same content in an npz container."""
         self._sync_from_device()
+        d = os.path.dirname(str(filepath))
+        if d:
+            os.makedirs(d, exist_ok=True)
+        if str(filepath).endswith(('.h5', '.hdf5')):
+            from . import h5io
+            h5io.write_keras_h5(str(filepath), self.model_config, self._h5_layer_weights(),
+                                training_config=self._training_config(),
+                                optimizer_weights=self._optimizer_state() if include_optimizer else None,
+                                keras_version=KERAS_VERSION)
+            return
         arrs = {'__model_config__': np.frombuffer(json.dumps(self.model_config).encode(), np.uint8),
                 '__keras_version__': np.frombuffer(KERAS_VERSION.encode(), np.uint8)}
         for k in self.weight_keys():
             arrs['w/' + k] = self._weights[k]
-        eng = self._engine
-        if eng is not None and eng.m is not None and self.optimizer is not None:
-            nm = type(self.optimizer).__name__
-            m = eng.m.cpu().numpy()
-            v = eng.v.cpu().numpy()
-            for k, (o, shp) in eng.layout.param_index.items():
-                sz = int(np.prod(shp))
-                arrs['o/%s/%s/m' % (nm, k)] = m[o:o + sz].reshape(shp)
-                arrs['o/%s/%s/v' % (nm, k)] = v[o:o + sz].reshape(shp)
-            arrs['o/%s/iter' % nm] = np.asarray(eng.iterations, np.int64)
-        d = os.path.dirname(str(filepath))
-        if d:
-            os.makedirs(d, exist_ok=True)
+        for n, a in (self._optimizer_state() or []) if include_optimizer else []:
+            arrs['o/' + n[:-2]] = a
         with open(filepath, 'wb') as fh:
             np.savez(fh, **arrs)
+
+    def _set_optimizer_state(self, opt_weights):
+        """Stage a legacy optimizer state ({'Adam/iter': n, 'Adam/<key>/m': arr, ...}) to be
+        loaded into the device buffers when the engine is created (Keras restores it on
+        load_model(compile=True))."""
+        pend = {'iter': 0, 'm': {}, 'v': {}}
+        for n, a in opt_weights.items():
+            parts = n.split('/')
+            if parts[-1] == 'iter':
+                pend['iter'] = int(np.asarray(a))
+            elif parts[-1] in ('m', 'v'):
+                pend[parts[-1]]['/'.join(parts[1:-1])] = np.asarray(a, np.float32)
+        self._pending_opt = pend
+        if self._engine is not None:
+            self._apply_pending_opt(self._engine)
+
+    def _apply_pending_opt(self, eng):
+        pend = getattr(self, '_pending_opt', None)
+        if not pend:
+            return
+        import torch
+        eng.iterations = pend['iter']
+        if pend['m']:
+            m = np.zeros(eng.n_train, np.float32)
+            v = np.zeros(eng.n_train, np.float32)
+            for k, (o, shp) in eng.layout.param_index.items():
+                n = int(np.prod(shp))
+                if k in pend['m']:
+                    m[o:o + n] = pend['m'][k].ravel()
+                    v[o:o + n] = pend['v'][k].ravel()
+            eng.m = torch.from_numpy(m).to(eng.device)
+            eng.v = torch.from_numpy(v).to(eng.device)
+        self._pending_opt = None
 
     def load_weights(self, filepath):
         m = load_model(filepath)
@@ -338,9 +435,28 @@ def model_from_config(model_config, weights, name=None):
     return Model(name=name or cfg.get('name'), _config=cfg, _weights=weights)
 
 
+def _compile_from(model, training_config, opt_state):
+    """Keras load_model(compile=True): re-create the optimizer from training_config (class and
+    hyper-parameters) and restore its state (iterations, m, v)."""
+    if not training_config or not isinstance(model, Model):
+        return model
+    oc = training_config.get('optimizer_config') or {}
+    cls = {'SGD': O.SGD, 'Adam': O.Adam, 'Adamax': O.Adamax}.get(oc.get('class_name'))
+    if cls is None:
+        return model
+    c = dict(oc.get('config', {}))
+    kw = {k: c[k] for k in ('learning_rate', 'beta_1', 'beta_2', 'epsilon', 'name') if k in c}
+    model.compile(optimizer=cls(**kw), loss='mse',
+                  metrics=['mae'] if training_config.get('metrics') else None)
+    if opt_state:
+        model._set_optimizer_state(opt_state)
+    return model
+
+
 def load_model(filepath, compile=True, **kw):
     """Load a model saved by Model.save, a converted fixture (<id>.json + <id>.npz), or a Keras
-    ``.h5`` file (via hpe.h5io)."""
+    ``.h5`` file (via hpe.h5io); with compile=True the optimizer and its state come back too
+    (test.py:31 loads the reference's checkpoints this way)."""
     p = str(filepath)
     if p.endswith('.json') or (not os.path.exists(p) and os.path.exists(p + '.json')):
         base = p[:-5] if p.endswith('.json') else p
@@ -354,8 +470,9 @@ def load_model(filepath, compile=True, **kw):
         magic = fh.read(8)
     if magic.startswith(b'\x89HDF'):
         from . import h5io
-        mc, w = h5io.read_keras_h5(p)
-        return model_from_config(mc, w)
+        mc, w, opt = h5io.read_keras_h5(p, with_optimizer=True)
+        m = model_from_config(mc, w)
+        return _compile_from(m, h5io.read_training_config(p), opt) if compile else m
     z = np.load(p, allow_pickle=False)
     mc = json.loads(bytes(z['__model_config__']).decode())
     w = {k[2:]: z[k] for k in z.files if k.startswith('w/')}

@@ -88,3 +88,164 @@ def test_gpu_predict_from_h5_matches_oracle(rid):
     x = np.maximum(0.0, 0.6 * np.random.default_rng(1).standard_normal((40, 1, 1, c)) - 0.3).astype(np.float32)
     ref = K.Graph(mc, w).forward(x).detach().numpy()
     np.testing.assert_allclose(m.predict(x), ref, rtol=1e-5, atol=1e-4)
+
+
+# ---- writer (Model.save('x.h5'), ModelCheckpoint) ---------------------------------------------
+def _layers_of(mc, w):
+    out = []
+    for l in mc['config']['layers']:
+        ln = l['name']
+        ws = [(k[len(ln) + 1:] + ':0' if l['class_name'] == 'Functional' else k + ':0', a)
+              for k, a in w.items() if k.startswith(ln + '/')]
+        out.append((ln, ws))
+    return out
+
+
+def _tree(f, addr=None, path=''):
+    """{path: sorted attr names} of every object in a file (our reader), for structure checks."""
+    addr = f.root if addr is None else addr
+    out = {path or '/': sorted(f.attrs(addr))}
+    ch = f.children(addr)
+    for n, a in (ch or {}).items():
+        out.update(_tree(f, a, path + '/' + n))
+    return out
+
+
+@pytest.mark.parametrize('rid', IDS)
+def test_writer_roundtrip_fixture(rid, tmp_path):
+    src = os.path.join(H5, rid + '.h5')
+    mc, w, opt = h5io.read_keras_h5(src, with_optimizer=True)
+    out = str(tmp_path / 'x.h5')
+    h5io.write_keras_h5(out, mc, _layers_of(mc, w), h5io.read_training_config(src),
+                        [(k + ':0', v) for k, v in opt.items()] or None)
+    mc2, w2, opt2 = h5io.read_keras_h5(out, with_optimizer=True)
+    assert mc2 == mc and list(w2) == list(w)
+    for k in w:
+        np.testing.assert_array_equal(w2[k], w[k])
+        assert w2[k].dtype == w[k].dtype
+    assert list(opt2) == list(opt)
+    for k in opt:
+        assert np.asarray(opt2[k]).shape == np.asarray(opt[k]).shape
+        np.testing.assert_array_equal(opt2[k], opt[k])
+    assert h5io.read_training_config(out) == h5io.read_training_config(src)
+    # same objects and attribute names as the file Keras wrote (our writer adds the
+    # top_level_model_weights group Keras 2.13.1 writes; older files may lack it)
+    t_src, t_out = _tree(h5io._File(src)), _tree(h5io._File(out))
+    t_out.pop('/model_weights/top_level_model_weights', None)
+    t_src.pop('/model_weights/top_level_model_weights', None)
+    assert t_out == t_src
+
+
+def _h5py_python():
+    p = '/opt/conda/bin/python3.9'
+    if not os.path.exists(p):
+        return None
+    import subprocess
+    r = subprocess.run([p, '-c', 'import h5py'], capture_output=True)
+    return p if r.returncode == 0 else None
+
+
+@pytest.mark.skipif(_h5py_python() is None, reason='no h5py interpreter (build container only)')
+def test_writer_output_reads_in_h5py(tmp_path):
+    """Independent check with libhdf5 itself (h5py 3.3 of /opt/conda, present in the build
+    container only): every attribute and dataset of a written checkpoint reads back."""
+    import subprocess
+    src = os.path.join(H5, '0g73t16n.h5')
+    mc, w, opt = h5io.read_keras_h5(src, with_optimizer=True)
+    out = str(tmp_path / 'x.h5')
+    h5io.write_keras_h5(out, mc, _layers_of(mc, w), h5io.read_training_config(src),
+                        [(k + ':0', v) for k, v in opt.items()])
+    script = r'''
+import h5py, json, sys, numpy as np
+f = h5py.File(sys.argv[1], 'r')
+res = {'attrs': {k: str(v) for k, v in f.attrs.items()}, 'data': {}, 'gattrs': {}}
+def visit(n, o):
+    if isinstance(o, h5py.Dataset):
+        a = np.asarray(o); res['data'][n] = [list(a.shape), str(a.dtype), float(np.asarray(a, np.float64).sum())]
+    else:
+        res['gattrs'][n] = {k: [str(x) for x in np.atleast_1d(v)] for k, v in o.attrs.items()}
+f.visititems(visit)
+print(json.dumps(res))
+'''
+    r = subprocess.run([_h5py_python(), '-c', script, out], capture_output=True, text=True, check=True)
+    res = json.loads(r.stdout)
+    assert json.loads(res['attrs']['model_config']) == mc
+    assert res['attrs']['keras_version'] == '2.13.1' and res['attrs']['backend'] == 'tensorflow'
+    assert res['gattrs']['model_weights']['layer_names'] == [l['name'] for l in mc['config']['layers']]
+    for k, a in w.items():
+        ln = k.split('/')[0]
+        shape, dt, s = res['data']['model_weights/%s/%s:0' % (ln, k)]
+        assert tuple(shape) == a.shape and dt == 'float32'
+        assert s == pytest.approx(float(a.astype(np.float64).sum()), rel=1e-12, abs=1e-12)
+    shape, dt, s = res['data']['optimizer_weights/Adam/iter:0']
+    assert shape == [] and dt == 'int64' and s == float(opt['Adam/iter'])
+
+
+def test_model_save_h5_and_load_model_compile(tmp_path):
+    """Model.save('<id>.h5') (ModelCheckpoint's format) -> load_model: same graph, weights,
+    optimizer class / hyper-parameters (float32-rounded like Keras's training_config)."""
+    import hpe
+    from hpe import keras
+    hpe.set_seed(3)
+    keras.backend.clear_session()
+    inp = keras.Input(shape=(None, None, 96))
+    h = keras.layers.Conv2D(16, 1, activation='tanh')(inp)
+    out = keras.layers.Conv2D(3, 1)(keras.layers.SpatialDropout2D(0.1)(h))
+    m = keras.Model(inp, out)
+    m.compile(optimizer=keras.optimizers.Adamax(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    p = str(tmp_path / 'run' / 'abc12345.h5')
+    m.save(p)
+    assert open(p, 'rb').read(8) == b'\x89HDF\r\n\x1a\n'
+    m2 = hpe.load_model(p)
+    assert m2.model_config == m.model_config
+    for a, b in zip(m.get_weights(), m2.get_weights()):
+        np.testing.assert_array_equal(a, b)
+    assert type(m2.optimizer).__name__ == 'Adamax'
+    assert m2.optimizer.learning_rate == float(np.float32(2.8e-4))
+    tc = h5io.read_training_config(p)
+    assert tc['optimizer_config']['config']['learning_rate'] == float(np.float32(2.8e-4))
+    _, _, opt = h5io.read_keras_h5(p, with_optimizer=True)
+    assert list(opt) == ['Adamax/iter']  # no steps taken yet: iterations only
+    m3 = hpe.load_model(p, compile=False)
+    assert m3.optimizer is None
+
+
+def test_load_model_restores_reference_adam_state():
+    import hpe
+    m = hpe.load_model(os.path.join(H5, '0g73t16n.h5'))
+    assert type(m.optimizer).__name__ == 'Adam'
+    _, _, opt = h5io.read_keras_h5(os.path.join(H5, '0g73t16n.h5'), with_optimizer=True)
+    assert m._pending_opt['iter'] == int(opt['Adam/iter'])
+    # re-saving without touching the device writes the same optimizer state back
+    state = dict(m._optimizer_state())
+    for k, v in opt.items():
+        np.testing.assert_array_equal(state[k + ':0'], v)
+
+
+@pytest.mark.gpu
+def test_gpu_checkpoint_resume_is_exact(tmp_path):
+    """fit 2 epochs, save .h5 (weights + Adam m/v/iter), load, fit 2 more == fit 4 straight."""
+    import hpe
+    from hpe import keras
+    rng = np.random.default_rng(5)
+    x = np.maximum(0.0, 0.6 * rng.standard_normal((300, 1, 1, 96)) - 0.3).astype(np.float32)
+    y = (20 * rng.standard_normal((300, 1, 1, 3))).astype(np.float32)
+
+    def build():
+        hpe.set_seed(11)
+        keras.backend.clear_session()
+        inp = keras.Input(shape=(None, None, 96))
+        h = keras.layers.Conv2D(32, 1, activation='tanh', kernel_regularizer=keras.regularizers.l2(1e-3))(inp)
+        m = keras.Model(inp, keras.layers.Conv2D(3, 1)(h))
+        m.compile(optimizer=keras.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
+        return m
+    a = build()
+    a.fit(x, y, batch_size=64, epochs=4, shuffle=False, verbose=0)
+    b = build()
+    b.fit(x, y, batch_size=64, epochs=2, shuffle=False, verbose=0)
+    p = str(tmp_path / 'ck.h5')
+    b.save(p)
+    c = hpe.load_model(p)
+    c.fit(x, y, batch_size=64, epochs=2, shuffle=False, verbose=0)
+    for wa, wc in zip(a.get_weights(), c.get_weights()):
+        np.testing.assert_array_equal(wa, wc)
