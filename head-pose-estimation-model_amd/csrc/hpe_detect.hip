@@ -194,3 +194,50 @@ extern "C" int hpe_detect(const float* cls0, const float* cls1, const float* loc
   if (e != hipSuccess) return hpe_fail(HPE_ERUNTIME, "hpe_detect launch: %s", hipGetErrorString(e));
   return HPE_OK;
 }
+
+// ---- feature-dataset extraction ------------------------------------------------
+// For each of the first k kept detections of a frame, the regressor input its pose came from
+// (blazeFaceDetectorH5.py:342-353): detection d < 512 -> re_lu_10 cell d / 2 of the 16 x 16 tap,
+// otherwise re_lu_15 cell (d - 512) / 6 of the 8 x 8 tap.  One workgroup per (frame, slot), one
+// float4 per lane (C0, C1 multiples of 4); the unused tap's row and empty slots are zero-filled and
+// src = 0 (front) / 1 (back) / -1 (no detection).
+__global__ void __launch_bounds__(64) gather_features_kernel(const int32_t* count, const int32_t* det_index,
+                                                               int max_faces, int k, const float* tap0, int c0,
+                                                               const float* tap1, int c1, float* feat0,
+                                                               float* feat1, int32_t* src) {
+  const int64_t img = blockIdx.x / k;
+  const int j = blockIdx.x - (int)(img * k);
+  const int t = threadIdx.x;
+  const int64_t o = img * k + j;
+  const int ns = count[img];
+  int d = -1;
+  if (j < ns) d = det_index[img * max_faces + j];
+  const float4* s0 = nullptr;
+  const float4* s1 = nullptr;
+  if (d >= 0 && d < DET_N0) s0 = (const float4*)(tap0 + (img * 256 + (d >> 1)) * c0);
+  if (d >= DET_N0) s1 = (const float4*)(tap1 + (img * 64 + (d - DET_N0) / 6) * c1);
+  float4* f0 = (float4*)(feat0 + o * c0);
+  float4* f1 = (float4*)(feat1 + o * c1);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = t; i < c0 / 4; i += 64) f0[i] = s0 ? s0[i] : z;
+  for (int i = t; i < c1 / 4; i += 64) f1[i] = s1 ? s1[i] : z;
+  if (t == 0) src[o] = d < 0 ? -1 : (d < DET_N0 ? 0 : 1);
+}
+
+extern "C" int hpe_gather_features(const int32_t* count, const int32_t* det_index, int64_t n_images,
+                                   int32_t max_faces, int32_t k, const float* tap0, int32_t c0, const float* tap1,
+                                   int32_t c1, float* feat0, float* feat1, int32_t* src, void* stream) {
+  if (!count || !det_index || !tap0 || !tap1 || !feat0 || !feat1 || !src)
+    return hpe_fail(HPE_EINVAL, "hpe_gather_features: null argument");
+  if (max_faces <= 0 || k <= 0 || k > max_faces)
+    return hpe_fail(HPE_EINVAL, "hpe_gather_features: need 0 < k <= max_faces (k %d, max_faces %d)", k, max_faces);
+  if (c0 <= 0 || c1 <= 0 || (c0 & 3) || (c1 & 3))
+    return hpe_fail(HPE_EINVAL, "hpe_gather_features: channel counts %d / %d must be positive multiples of 4", c0, c1);
+  if (n_images <= 0) return HPE_OK;
+  if (n_images * k > 0x7fffffff) return hpe_fail(HPE_EINVAL, "hpe_gather_features: batch too large");
+  hipLaunchKernelGGL(gather_features_kernel, dim3((unsigned)(n_images * k)), dim3(64), 0, (hipStream_t)stream,
+                     count, det_index, (int)max_faces, (int)k, tap0, (int)c0, tap1, (int)c1, feat0, feat1, src);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hpe_fail(HPE_ERUNTIME, "hpe_gather_features launch: %s", hipGetErrorString(e));
+  return HPE_OK;
+}

@@ -28,6 +28,8 @@ SIGNATURES = {
     'hpe_blazeface_forward': (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     'hpe_detect': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _i32, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
+    'hpe_gather_features': (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp,
+                                           _vp, _vp]),
     'hpe_se_gate': (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
                                    _vp]),
     'hpe_seg_mean': (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp]),

@@ -10,8 +10,9 @@ import time
 
 class _Run:
     def __init__(self, project, config, notes, tags):
-        self.id = ''.join(random.Random(time.time_ns()).choice(string.ascii_lowercase + string.digits)
-                          for _ in range(8))
+        # a sweep controller (hpe.sweep) names the run so it can read the summary back
+        self.id = os.environ.get('HPE_RUN_ID') or ''.join(
+            random.Random(time.time_ns()).choice(string.ascii_lowercase + string.digits) for _ in range(8))
         self.project, self.config, self.notes, self.tags = project, dict(config or {}), notes, tags
         self.summary = {}
         d = os.environ.get('HPE_RUN_DIR', 'runs')
@@ -43,3 +44,19 @@ def init(project=None, config=None, notes='', tags=None, **kw):
 def log(d):
     if run is not None:
         run.log(d)
+
+
+def read_summary(path):
+    """The last summary record of a run's JSON-lines file ({} if the run never finished)."""
+    out = {}
+    if not os.path.exists(path):
+        return out
+    with open(path) as fh:
+        for line in fh:
+            try:
+                rec = json.loads(line)
+            except ValueError:
+                continue
+            if rec.get('event') == 'summary':
+                out = {k: v for k, v in rec.items() if k != 'event'}
+    return out

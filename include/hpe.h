@@ -130,6 +130,16 @@ int hpe_detect(const float *cls0, const float *cls1, const float *loc0, const fl
                float iou_threshold, int32_t max_faces, int32_t *count, int32_t *det_index, float *scores,
                double *boxes, double *keypoints, float *poses, void *stream);
 
+/* Feature-dataset extraction (the *_features_88|96_<t>_<k>.npz files of
+ * FeatureMaps-Datasets/, whose extractor is outside the reference, JoinModels.py:114 taps re_lu_10 /
+ * re_lu_15): for the first k kept detections of each frame (hpe_detect outputs), the regressor input
+ * that detection's pose was computed from, following the pose gather at blazeFaceDetectorH5.py:342-353
+ * — d < 512: tap0 (n,16,16,c0) cell d/2; else tap1 (n,8,8,c1) cell (d-512)/6.  Outputs (device):
+ * feat0 (n,k,c0), feat1 (n,k,c1) (the other tap's row zero), src (n,k) int32 0 / 1 / -1 (empty). */
+int hpe_gather_features(const int32_t *count, const int32_t *det_index, int64_t n_images, int32_t max_faces,
+                        int32_t k, const float *tap0, int32_t c0, const float *tap1, int32_t c1, float *feat0,
+                        float *feat1, int32_t *src, void *stream);
+
 const char *hpe_last_error(void);
 
 /* Attention heads on H x W > 1 feature maps: the two stages that are not

@@ -113,3 +113,26 @@ def detect_frame(cls0, cls1, loc0, loc1, pose_front, pose_back, score_threshold=
             poses.append(pose_back[cell // 8, cell % 8])
     poses = np.asarray(poses, np.float32).reshape(-1, 3)
     return dict(det_index=det, scores=scores[sel], boxes=boxes[sel], keypoints=kps[sel], poses=poses)
+
+
+def gather_features(det_index, tap_front, tap_back, k=1):
+    """Feature-dataset extraction for one frame — TEST INFRASTRUCTURE.
+
+    For each of the first k kept detections, the regressor input its pose came from: the same cell
+    arithmetic as the pose gather at blazeFaceDetectorH5.py:342-353 applied to the tapped maps
+    (JoinModels.py:114 taps re_lu_10 -> tap_front (16,16,C0), re_lu_15 -> tap_back (8,8,C1)).
+    Returns (feat_front (k,C0), feat_back (k,C1), src (k,) 0 front / 1 back / -1 empty)."""
+    c0, c1 = tap_front.shape[-1], tap_back.shape[-1]
+    f0 = np.zeros((k, c0), np.float32)
+    f1 = np.zeros((k, c1), np.float32)
+    src = np.full(k, -1, np.int32)
+    for j, d in enumerate(list(det_index)[:k]):
+        if d < 512:
+            cell = d // 2
+            f0[j] = tap_front[cell // 16, cell % 16]
+            src[j] = 0
+        else:
+            cell = (d - 512) // 6
+            f1[j] = tap_back[cell // 8, cell % 8]
+            src[j] = 1
+    return f0, f1, src
