@@ -41,7 +41,6 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; 
 // channels replace four v_mfma_f32_32x32x2_f32 (64 cycles each) per 8 channels.  The W^T table
 // holds each quad of weights as {hi[4], lo[4]} (16 B, the footprint of the fp32 quad it replaces).
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ h4 to_h4(f32x4 v) {
   return h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
 }

@@ -43,6 +43,8 @@ __device__ __forceinline__ float cact(int act, float z) {
 // O_AUX1 b2, O_AUX2 W3, O_TBASE b3, O_EACT act1, O_FLAGS act2, O_MODE act3, O_TCOUNT N3 (= 3)
 template <int A1, int A2, int A3, int GATHER>
 __global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
+  // guarded fallback of chain_split_kernel: runs only when that launch flagged a non-finite tile
+  if (args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
@@ -176,6 +178,162 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
   }
 }
 
+
+// The same chain on fp16 MFMA at fp32 accuracy (split8 / mfma3, hpe_common.h): layer 1 as six
+// K-steps of three v_mfma_f32_32x32x16_f16 (576 MFMA cycles per 32-row tile instead of 3,072 on
+// v_mfma_f32_32x32x2_f32), layer 2 as two, the head on the VALU in fp32 as above.  With the MFMA
+// work cut 5x the kernel is bound by the X stream alone.  A tile whose accumulators come out
+// non-finite (an input or activation outside the fp16 range) sets the guard word; the exact-fp32
+// kernel launched behind it then recomputes the whole launch.
+template <int A1, int A2, int A3, int GATHER>
+__global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int* prog = args.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int Cin = o[O_K], F1 = o[O_N], F2 = o[O_AUX3];
+  const int act1 = o[O_EACT], act2 = o[O_FLAGS], act3 = o[O_MODE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const float* P_ = args.params;
+  float* tw2 = lds;
+  float* tb1 = tw2 + 1024;
+  float* tb2 = tb1 + 32;
+  float* tw3 = tb2 + 32;
+  float* tb3 = tw3 + 128;
+  float* xs = lds + CHAIN_TAB + wave * CHAIN_XF;
+  const int Fh = F2 > 0 ? F2 : F1;
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+    const int nn = i >> 5, m = i & 31;
+    tw2[i] = (F2 > 0 && nn < F1 && m < F2) ? P_[o[O_AUX0] + nn * F2 + m] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) {
+    tb1[i] = (i < F1 && o[O_BIAS] >= 0) ? P_[o[O_BIAS] + i] : 0.f;
+    tb2[i] = (F2 > 0 && i < F2 && o[O_AUX1] >= 0) ? P_[o[O_AUX1] + i] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    const int nn = i >> 2, j = i & 3;
+    tw3[i] = (nn < Fh && j < 3) ? P_[o[O_AUX2] + nn * 3 + j] : 0.f;
+  }
+  if (threadIdx.x < 4) tb3[threadIdx.x] = (threadIdx.x < 3 && o[O_TBASE] >= 0) ? P_[o[O_TBASE] + threadIdx.x] : 0.f;
+
+  // A of layer 1: W1^T[n = l32][k], K-step s holds k = 16 s + 8 half + j (j = 0..7)
+  h8 w1h[6], w1l[6];
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    f32x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * half + j;
+      const float t = P_[o[O_W] + (size_t)min(k, Cin - 1) * F1 + min(l32, F1 - 1)];
+      v[j] = (k < Cin && l32 < F1) ? t : 0.f;
+    }
+    split8(v, w1h[s], w1l[s]);
+  }
+  __syncthreads();
+  // A of layer 2: W2^T[m = l32][n], in the k order of an accumulator used as the B operand:
+  // element j of K-step s of lane half h <-> hidden unit 16 s + 8 (j >> 2) + 4 h + (j & 3)
+  h8 w2h[2], w2l[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    f32x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tw2[(16 * s + 8 * (j >> 2) + 4 * half + (j & 3)) * 32 + l32];
+    split8(v, w2h[s], w2l[s]);
+  }
+  float b1r[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) b1r[g] = tb1[(g & 3) + 8 * (g >> 2) + 4 * half];
+
+  const int64_t nrows = args.nrows;
+  const int64_t ntiles = (nrows + 31) / 32;
+  const int P = args.P;
+  const int64_t gw = (int64_t)blockIdx.x * CHAIN_NW + wave;
+  const int64_t nw = (int64_t)gridDim.x * CHAIN_NW;
+  bool bad = false;
+  for (int64_t tile = gw; tile < ntiles; tile += nw) {
+    const int64_t row0 = tile * 32;
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
+    const float* xt = args.x + row0 * Cin;
+#pragma unroll
+    for (int pc = 0; pc < 12; ++pc) {
+      const int slot = pc * 64 + lz;
+      const int r = slot / 24, ph = slot - r * 24;
+      const int c = csw(r, ph);
+      const int cc = 4 * c < Cin ? c : 0;
+      const int rr = min(r, last);
+      const float* src;
+      if (GATHER) {
+        const int64_t R = row0 + rr;
+        const int64_t img = R / P, pos = R - img * P;
+        src = args.x + ((int64_t)args.idx[img] * P + pos) * Cin + 4 * cc;
+      } else {
+        src = xt + (rr * Cin + 4 * cc);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + pc * 256), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- layer 1: B = X^T, lane (row l32, half h) holds X[row][16 s + 8 h .. + 8) ----
+    const float* xr = xs + l32 * 96;
+    const int sw = (l32 >> 1) & 7;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int c0 = 4 * s + 2 * half;
+      const f32x4 a0 = *(const f32x4*)(xr + 4 * (c0 ^ sw));
+      const f32x4 a1 = *(const f32x4*)(xr + 4 * ((c0 + 1) ^ sw));
+      h8 xh, xl;
+      split8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, xh, xl);
+      acc = mfma3(w1h[s], w1l[s], xh, xl, acc);
+    }
+    float chk = sum16(acc);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, acc[g] + b1r[g]);
+    int toff = 0;
+    asm volatile("" : "+v"(toff));
+    // ---- layer 2 (optional): B = A1^T straight from the accumulator registers 8 s .. 8 s + 7 ----
+    f32x16 h = acc;
+    if (F2 > 0) {
+      f32x16 acc2 = {};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        h8 ah, al;
+        split8(f32x8{acc[8 * s + 0], acc[8 * s + 1], acc[8 * s + 2], acc[8 * s + 3],
+                     acc[8 * s + 4], acc[8 * s + 5], acc[8 * s + 6], acc[8 * s + 7]}, ah, al);
+        acc2 = mfma3(w2h[s], w2l[s], ah, al, acc2);
+      }
+      chk += sum16(acc2);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
+        acc2[g] = cact<A2>(act2, acc2[g] + tb2[toff + mm]);
+      }
+      h = acc2;
+    }
+    bad |= !(fabsf(chk) <= 3.0e38f);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int nn = (g & 3) + 8 * (g >> 2) + 4 * half;
+      const f32x4 w = *(const f32x4*)(tw3 + toff + nn * 4);
+      s0 = fmaf(h[g], w.x, s0);
+      s1 = fmaf(h[g], w.y, s1);
+      s2 = fmaf(h[g], w.z, s2);
+    }
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const int64_t R = row0 + l32;
+    if (half == 0 && R < nrows) {
+      float* yp = args.y + R * 3;
+      yp[0] = cact<A3>(act3, s0 + tb3[0]);
+      yp[1] = cact<A3>(act3, s1 + tb3[1]);
+      yp[2] = cact<A3>(act3, s2 + tb3[2]);
+    }
+  }
+  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 typedef void (*chain_fn)(Args);
 
 int chain_supported(const int* w) {
@@ -188,13 +346,34 @@ int chain_lds_bytes() { return (CHAIN_TAB + CHAIN_NW * CHAIN_XF) * 4; }
 
 int chain_grid_cap(int n_cu) { return n_cu; }  // one 12-wave workgroup per CU (LDS ~149 KiB)
 
-int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
-  const int* o = w + w[H_OPS_OFF];
+template <int A1, int A2, int A3, int G>
+struct ChainExact { static constexpr chain_fn f = chain_fwd_kernel<A1, A2, A3, G>; };
+template <int A1, int A2, int A3, int G>
+struct ChainSplit { static constexpr chain_fn f = chain_split_kernel<A1, A2, A3, G>; };
+
+template <template <int, int, int, int> class K>
+static chain_fn pick(const int* o, bool gather) {
   const bool tt_l = o[O_EACT] == ACT_TANH && (o[O_AUX3] == 0 || o[O_FLAGS] == ACT_TANH) && o[O_MODE] == ACT_LINEAR;
-  chain_fn k = tt_l ? (a.idx ? chain_fwd_kernel<ACT_TANH, ACT_TANH, ACT_LINEAR, 1>
-                             : chain_fwd_kernel<ACT_TANH, ACT_TANH, ACT_LINEAR, 0>)
-                    : (a.idx ? chain_fwd_kernel<-1, -1, -1, 1> : chain_fwd_kernel<-1, -1, -1, 0>);
+  if (tt_l) return gather ? K<ACT_TANH, ACT_TANH, ACT_LINEAR, 1>::f : K<ACT_TANH, ACT_TANH, ACT_LINEAR, 0>::f;
+  return gather ? K<-1, -1, -1, 1>::f : K<-1, -1, -1, 0>::f;
+}
+
+static int launch_one(chain_fn k, const Args& a, int grid, hipStream_t s) {
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, chain_lds_bytes());
   hipLaunchKernelGGL(k, dim3(grid), dim3(CHAIN_NW * 64), chain_lds_bytes(), s, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// split kernel, then its exact-fp32 twin, which exits at once unless the split kernel flagged a
+// non-finite tile in this launch (guard == epoch)
+int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
+  const int* o = w + w[H_OPS_OFF];
+  const bool g = a.idx != nullptr;
+  if (hpe_exact_fp32() || !a.guard) {
+    Args e = a;
+    e.guard = nullptr;
+    return launch_one(pick<ChainExact>(o, g), e, grid, s);
+  }
+  if (launch_one(pick<ChainSplit>(o, g), a, grid, s)) return 2;
+  return launch_one(pick<ChainExact>(o, g), a, grid, s);
 }

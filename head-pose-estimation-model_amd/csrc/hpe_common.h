@@ -133,7 +133,41 @@ struct Args {
   int64_t img_off;
   float inv_count;
   uint64_t seed;
+  int* guard;        // fp16-split kernels: set to `epoch` when a tile's split overflowed (non-finite)
+  int epoch;         //   -> the exact-fp32 kernel of the same launch re-runs (guard == epoch)
 };
+
+// ------------------------------------------------------------------------------------------------
+// fp32 GEMMs on fp16 MFMA at fp32 accuracy ("3 x fp16 split"): a = a_hi + a_lo, b = b_hi + b_lo
+// with fp16 halves (a_lo = fp16(a - a_hi) is exact to 2^-22 |a|), a.b ~= a_hi.b_hi + a_hi.b_lo +
+// a_lo.b_hi (the dropped a_lo.b_lo is ~2^-22 relative), fp32 accumulate.  Three
+// v_mfma_f32_32x32x16_f16 (32 cycles each) per 16 of K replace eight v_mfma_f32_32x32x2_f32
+// (64 cycles each): 5.3x the MFMA rate of the exact-fp32 instruction.  Range: |a|, |b| < 65504
+// (an fp16 overflow makes the accumulator non-finite; kernels using this check it and hand the
+// launch to their exact-fp32 twin, see Args::guard).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split8(f32x8 v, h8& hi, h8& lo) {
+  hi = __builtin_convertvector(v, h8);
+  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), h8);
+}
+
+__device__ __forceinline__ f32x16 mfma3(h8 ah, h8 al, h8 bh, h8 bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sum16(const f32x16& a) {
+  float s0 = (a[0] + a[1]) + (a[2] + a[3]), s1 = (a[4] + a[5]) + (a[6] + a[7]);
+  float s2 = (a[8] + a[9]) + (a[10] + a[11]), s3 = (a[12] + a[13]) + (a[14] + a[15]);
+  return (s0 + s1) + (s2 + s3);
+}
+
+// hpe_set_exact_fp32(): 1 = exact-fp32 MFMA kernels only (hpe_rowprog.hip)
+bool hpe_exact_fp32();
 
 // fused 2-layer regressor kernel (hpe_mlp2.hip)
 int mlp2_supported(const int* words);

@@ -20,6 +20,7 @@
 // autodiff of Keras' fit (train_96.py:175).  Optimizers: Keras legacy SGD/Adam/Adamax.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -770,9 +771,26 @@ struct hpe_program {
   int* words;  // host copy (fused-kernel geometry)
   int n_cu;
   int grid_cap;
+  int64_t n_words;
+  mutable int epoch;  // guarded (fp16-split) launches: guard word = dwords[n_words]
 };
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
+
+static int g_exact = -1;  // -1: not yet read from HPE_EXACT_FP32
+bool hpe_exact_fp32() {
+  if (g_exact < 0) {
+    const char* e = getenv("HPE_EXACT_FP32");
+    g_exact = e && e[0] == '1';
+  }
+  return g_exact == 1;
+}
+
+extern "C" int hpe_set_exact_fp32(int on) {
+  const int prev = hpe_exact_fp32() ? 1 : 0;
+  g_exact = on ? 1 : 0;
+  return prev;
+}
 
 typedef void (*kfn_t)(Args);
 
@@ -812,9 +830,12 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   memcpy(p->hdr, words, sizeof(p->hdr));
   p->words = new int[n_words];
   memcpy(p->words, words, n_words * sizeof(int32_t));
-  hipError_t e = hipMalloc(&p->dwords, n_words * sizeof(int32_t));
+  p->n_words = n_words;
+  p->epoch = 0;
+  hipError_t e = hipMalloc(&p->dwords, (n_words + 1) * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
-  e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
+  e = hipMemset(p->dwords + n_words, 0, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) { hipFree(p->dwords); delete p; return fail(HPE_ERUNTIME, "hipMemcpy: %s", hipGetErrorString(e)); }
   int dev = 0;
   hipGetDevice(&dev);
@@ -863,6 +884,9 @@ extern "C" size_t hpe_workspace_size(const hpe_program* p, int64_t n_rows) {
 
 static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   const int grid = hpe_launch_grid(p, nrows);
+  a.guard = p->dwords + p->n_words;
+  a.epoch = ++p->epoch;
+  if (a.epoch <= 0) a.epoch = p->epoch = 1;
   if (p->hdr[H_KIND] == KIND_MLP2) {
     if (mlp2_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "mlp2 launch: %s", hipGetErrorString(hipGetLastError()));
     return HPE_OK;

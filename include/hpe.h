@@ -142,6 +142,14 @@ int hpe_gather_features(const int32_t *count, const int32_t *det_index, int64_t 
 
 const char *hpe_last_error(void);
 
+/* Precision of the regressor GEMMs (process-wide; returns the previous setting).  Default 0: the
+ * fused kernels run their fp32 GEMMs as three fp16 MFMAs per product (hi/lo split, fp32
+ * accumulate, ~2^-22 relative per product; csrc/hpe_common.h mfma3), and a launch whose split
+ * overflows fp16 (|value| >= 65504) is recomputed by the exact-fp32 kernel automatically.
+ * 1: exact-fp32 MFMA (v_mfma_f32_32x32x2_f32) only.  The environment variable HPE_EXACT_FP32=1
+ * sets the initial value. */
+int hpe_set_exact_fp32(int on);
+
 /* Attention heads on H x W > 1 feature maps: the two stages that are not
  * row-local.  Replace the TF kernels behind GlobalAveragePooling2D -> Dense -> Dense -> Multiply
  * (Model-88/attention_model.py:34-38, :78-82) and behind MultiHeadAttention's softmax(QK^T)V over

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared():
     with open(os.path.join(ROOT, 'include', 'hpe.h')) as fh:
         src = fh.read()
-    return set(re.findall(r'^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(hpe_[a-z_]+)\s*\(', src, re.M))
+    return set(re.findall(r'^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(hpe_[a-z_0-9]+)\s*\(', src, re.M))
 
 
 def test_header_declares_expected_entry_points():

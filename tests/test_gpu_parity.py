@@ -162,3 +162,39 @@ def test_chain_forward_ragged_and_gather(rid):
         got = eng.forward(torch.from_numpy(x.reshape(-1, c)).cuda(), P,
                           idx=torch.from_numpy(idx).cuda()).cpu().numpy()
         np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL, err_msg='P=%d' % P)
+
+
+def test_chain_split_precision_and_overflow_guard():
+    """The chain kernel runs its GEMMs as fp16 hi/lo splits (csrc/hpe_common.h mfma3): its error
+    against the float64 oracle stays at the exact-fp32 kernel's level, and inputs outside the fp16
+    range (a feature >= 65504) are recomputed by the exact-fp32 twin (guard word), not mangled."""
+    from hpe import _lib
+    from hpe.engine import Engine
+    mc, w = fixture('hrchr82r')
+    eng = Engine(mc, w)
+    g = K.Graph(mc, w)
+    n = 100_003
+    x = features(n, 96, seed=11)
+    ref = g.forward(x).detach().numpy().reshape(-1, 3)
+    xt = torch.from_numpy(x.reshape(n, 96)).cuda()
+    lib = _lib.load()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        exact = eng.forward(xt, 1).cpu().numpy()
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    split = eng.forward(xt, 1).cpu().numpy()
+    e_exact = float(np.abs(exact - ref).max())
+    e_split = float(np.abs(split - ref).max())
+    print('max |err| vs float64 oracle: exact fp32 %.3e, fp16-split %.3e' % (e_exact, e_split))
+    assert e_split <= 4 * e_exact + 2e-6, (e_split, e_exact)
+    np.testing.assert_allclose(split, ref, rtol=RTOL, atol=ATOL)
+    xo = x.reshape(n, 96).copy()
+    xo[5, 3] = 1.0e5
+    xo[70_000, 10] = -7.0e4
+    refo = g.forward(xo.reshape(n, 1, 1, 96)).detach().numpy().reshape(-1, 3)
+    got = eng.forward(torch.from_numpy(xo).cuda(), 1).cpu().numpy()
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, refo, rtol=RTOL, atol=ATOL)
+    # the next launch (new epoch) is back on the split path and still right
+    np.testing.assert_allclose(eng.forward(xt, 1).cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
