@@ -163,8 +163,21 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
 }
 
 // NWM: launch bound in waves (12: any width <= 384, 168-VGPR budget; 4: F <= 128, 256 budget)
-template <int KH, int ACT1, bool DROP, int NWM>
+// SPLIT: both GEMMs on fp16 MFMA at fp32 accuracy (split8 / mfma3, hpe_common.h), same registers:
+//   forward  Z1 = X.W1: 6 K-steps of three v_mfma_f32_32x32x16_f16 (576 MFMA cycles per wave per
+//            tile instead of 48 x 64 = 3,072); K-step s, lane half h, element j <-> channel
+//            KH h + 8 s + j, so a lane splits 8 contiguous X floats of its row (two ds_read_b128) and
+//            W1 sits in registers as hi / lo fp16 B fragments (48 VGPRs, as the fp32 W1 slice);
+//   dW1 += X^T.dZ1: per 32-channel block two K-steps of three (576 instead of 3,072), the same 16
+//            X^T reads per block as the fp32 path, split in registers, dZ1 split once per tile.
+//   Loss gradients are carried unnormalised (2 (p - y): inside the fp16 range; the normalised
+//   ones underflow it) and the workgroup's partials are scaled by inv_count at the flush.  A
+//   non-finite forward accumulator or dW1 block (an input, dZ1 or weight outside the fp16 range)
+//   sets the guard word; the exact instantiation launched behind this one then recomputes the
+//   step into the same slabs (and exits at once otherwise).
+template <int KH, int ACT1, bool DROP, int NWM, bool SPLIT>
 __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
+  if (!SPLIT && args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NKB = (2 * KH + 31) / 32;  // 32-row blocks of dW1 (input channels)
   constexpr int T = 32;
@@ -196,13 +209,29 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   const float* W2 = args.params + o[O_AUX0];
 
   // ---- register-resident weights of this wave's 32 hidden columns ----
-  float wreg[KH];
+  float wreg[SPLIT ? 1 : KH];
+  h8 wh[SPLIT ? 6 : 1], wl[SPLIT ? 6 : 1];
+  if constexpr (SPLIT) {
 #pragma unroll
-  for (int m = 0; m < KH; ++m) {
-    const int k = half * KH + m;
-    const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
-    wreg[m] = (k < Cin && nok) ? wv : 0.f;
+    for (int s = 0; s < 6; ++s) {
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = half * KH + 8 * s + j;
+        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
+        v[j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
+      }
+      split8(v, wh[s], wl[s]);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < KH; ++m) {
+      const int k = half * KH + m;
+      const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
+      wreg[m] = (k < Cin && nok) ? wv : 0.f;
+    }
   }
+  bool bad = false;
   const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
   // small tables in LDS rather than loop-carried VGPRs (the 12-wave variant is at its budget)
   for (int i = threadIdx.x; i < NCB * 128; i += NT) {
@@ -226,11 +255,11 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   // so its output index j (and its db2 accumulator) is the same in every tile
   const int NT3 = (NT / 3) * 3;
 
-  // pad columns [C_in, ceil8(C_in)) of both X buffers: never written by the staging, read by the
-  // forward MFMA against zero weights -> must hold zeros, not stale LDS
-  for (int i = threadIdx.x; i < 64 * 8; i += NT) {
-    const int r = i >> 3, c = Cin + (i & 7);
-    if (c < ((Cin + 7) & ~7)) xbuf[r * MLP2_XS + c] = 0.f;
+  // pad columns [C_in, 96) of both X buffers: never written by the staging, read by the forward
+  // MFMA against zero weights -> must hold zeros, not stale LDS
+  for (int i = threadIdx.x; i < 64 * 16; i += NT) {
+    const int r = i >> 4, c = Cin + (i & 15);
+    if (c < 96) xbuf[r * MLP2_XS + c] = 0.f;
   }
   __syncthreads();
   // tile -> (first image, row within it), advanced incrementally (no 64-bit division per tile)
@@ -261,16 +290,28 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     {
       const float* ap = xs + l32 * MLP2_XS + half * KH;
       f32x16 acc = {};
-      f32x4 an = *(const f32x4*)(ap);
+      if constexpr (SPLIT) {
 #pragma unroll
-      for (int m = 0; m < KH; m += 4) {
-        const f32x4 a = an;
-        if (m + 4 < KH) an = *(const f32x4*)(ap + m + 4);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wreg[m + 0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wreg[m + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wreg[m + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wreg[m + 3], acc, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < 6; ++s) {
+          const f32x4 a0 = *(const f32x4*)(ap + 8 * s), a1 = *(const f32x4*)(ap + 8 * s + 4);
+          h8 xh, xl;
+          split8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, xh, xl);
+          acc = mfma3(xh, xl, wh[s], wl[s], acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
+      } else {
+        f32x4 an = *(const f32x4*)(ap);
+#pragma unroll
+        for (int m = 0; m < KH; m += 4) {
+          const f32x4 a = an;
+          if (m + 4 < KH) an = *(const f32x4*)(ap + m + 4);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wreg[m + 0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wreg[m + 1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wreg[m + 2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wreg[m + 3], acc, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (DROP) {
         if (P >= 32) {  // two images at most: two hashes per lane per tile
@@ -352,7 +393,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
           const float err = p - lab[r * 4 + j];
           hacc[threadIdx.x * 4 + 0] = fmaf(err, err, hacc[threadIdx.x * 4 + 0]);
           hacc[threadIdx.x * 4 + 1] += fabsf(err);
-          g = 2.f * err * args.inv_count;
+          g = SPLIT ? 2.f * err : 2.f * err * args.inv_count;
         }
         if (train) {
           g = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr
@@ -368,10 +409,9 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 
     // ---- backward: dA1 = dZ2.W2^T, dZ1, dW2, db1 in registers; dW1 += X^T.dZ1 on MFMA ----
     {
-      float dz1[16];
       const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
+      // dZ1 of accumulator register g (row (g & 3) + 8 (g >> 2) + 4 h), dW2 / db1 on the way
+      auto dz_of = [&](int g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
         const f32x4 d = *(const f32x4*)(dz2 + r * 4);
         const float a = a1s[(wave * 16 + g) * 64 + lane];
@@ -388,61 +428,101 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
         dw2[1] = fmaf(a, d.y, dw2[1]);
         dw2[2] = fmaf(a, d.z, dw2[2]);
         db1 += gz;
-        dz1[g] = gz;
-        if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the dZ2 reads in flight
-      }
+        return gz;
+      };
+      if constexpr (SPLIT) {
+        // K-step s (rows 16 s + 8 (j >> 2) + 4 h + (j & 3)): dZ1 registers 8 s .. 8 s + 7 as the B
+        // operand, the matching X^T rows as A; one K-step at a time keeps the live set small
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        // X^T block: lane reads X[r(g)][k = 32 kb + l32]
-        const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
-        f32x16 acc = dw[kb];
-        auto xat = [&](int g) { return xp[((g & 3) + 8 * (g >> 2)) * MLP2_XS]; };
-        float x0 = xat(0), x1 = xat(1);
+        for (int s = 0; s < 2; ++s) {
+          f32x8 dv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            dv[j] = dz_of(8 * s + j);
+            if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+          h8 dh, dl;
+          split8(dv, dh, dl);
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) {
+            const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
+            f32x8 xv;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] = xp[(16 * s + 8 * (j >> 2) + (j & 3)) * MLP2_XS];
+            h8 th, tl;
+            split8(xv, th, tl);
+            dw[kb] = mfma3(th, tl, dh, dl, dw[kb]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      } else {
+        float dz1[16];
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          const float xv = x0;
-          x0 = x1;
-          if (g + 2 < 16) x1 = xat(g + 2);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, dz1[g], acc, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
+          dz1[g] = dz_of(g);
+          if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the dZ2 reads in flight
         }
-        dw[kb] = acc;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          // X^T block: lane reads X[r(g)][k = 32 kb + l32]
+          const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
+          f32x16 acc = dw[kb];
+          auto xat = [&](int g) { return xp[((g & 3) + 8 * (g >> 2)) * MLP2_XS]; };
+          float x0 = xat(0), x1 = xat(1);
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const float xv = x0;
+            x0 = x1;
+            if (g + 2 < 16) x1 = xat(g + 2);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, dz1[g], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          dw[kb] = acc;
+        }
       }
     }
   }
 
-  if (mode == MODE_FWD) return;
+  if (mode == MODE_FWD) {
+    if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // ---- flush this workgroup's partial gradients + loss sums ----
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
+  const float sc = SPLIT ? args.inv_count : 1.f;  // the split path carries unnormalised gradients
   __syncthreads();
   if (train) {
+    float chk = 0.f;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
+      if (SPLIT) chk += sum16(dw[kb]);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g];
+        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * sc;
       }
     }
+    if (SPLIT) bad |= !(fabsf(chk) <= 3.0e38f);
     const float tb = db1 + __shfl_xor(db1, 32, 64);
     float t2[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
     if (half == 0 && nok) {
-      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb;
+      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j];
+      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
     }
     // db2: per-thread accumulators of output j = tid % 3 -> fixed-order sum
     if (threadIdx.x < 3 && o[O_AUX1] >= 0) {
       float s = 0.f;
       for (int i = threadIdx.x; i < NT3; i += 3) s += hacc[i * 4 + 2];
-      ws[o[O_AUX1] + threadIdx.x] = s;
+      ws[o[O_AUX1] + threadIdx.x] = s * sc;
     }
     __syncthreads();
   }
+  if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float a = wave_sum(hacc[threadIdx.x * 4 + 0]), b = wave_sum(hacc[threadIdx.x * 4 + 1]);
   if (lane == 0) { red[wave] = a; red[MLP2_MAXW + wave] = b; }
   __syncthreads();
@@ -458,29 +538,31 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
-template <int KH, bool DROP, int NWM>
+template <int KH, bool DROP, int NWM, bool SPLIT>
 static mlp2_fn pick_act(int act, int act2) {
-  if (act2 != ACT_LINEAR) return mlp2_kernel<KH, -1, DROP, NWM>;
-  if (act == ACT_TANH) return mlp2_kernel<KH, ACT_TANH, DROP, NWM>;
-  if (act == ACT_SOFTSIGN) return mlp2_kernel<KH, ACT_SOFTSIGN, DROP, NWM>;
-  return mlp2_kernel<KH, -1, DROP, NWM>;
+  if (act2 != ACT_LINEAR) return mlp2_kernel<KH, -1, DROP, NWM, SPLIT>;
+  if (act == ACT_TANH) return mlp2_kernel<KH, ACT_TANH, DROP, NWM, SPLIT>;
+  if (act == ACT_SOFTSIGN) return mlp2_kernel<KH, ACT_SOFTSIGN, DROP, NWM, SPLIT>;
+  return mlp2_kernel<KH, -1, DROP, NWM, SPLIT>;
 }
 
-template <bool DROP>
+template <bool DROP, bool SPLIT>
 static mlp2_fn pick_d(int kh, int act, int act2, int ncb) {
   if (ncb <= 4) {
-    if (kh == 44) return pick_act<44, DROP, 4>(act, act2);  // 88-channel BlazeFace tap (Model-88)
-    if (kh == 48) return pick_act<48, DROP, 4>(act, act2);  // 96-channel tap (Model-96)
+    if (kh == 44) return pick_act<44, DROP, 4, SPLIT>(act, act2);  // 88-channel BlazeFace tap (Model-88)
+    if (kh == 48) return pick_act<48, DROP, 4, SPLIT>(act, act2);  // 96-channel tap (Model-96)
   }
-  if (kh == 44) return pick_act<44, DROP, MLP2_MAXW>(act, act2);
-  if (kh == 48) return pick_act<48, DROP, MLP2_MAXW>(act, act2);
+  if (kh == 44) return pick_act<44, DROP, MLP2_MAXW, SPLIT>(act, act2);
+  if (kh == 48) return pick_act<48, DROP, MLP2_MAXW, SPLIT>(act, act2);
   return nullptr;
 }
 
-static mlp2_fn pick(const int* w) {
+static mlp2_fn pick(const int* w, bool split = false) {
   const int* o = w + w[H_OPS_OFF];
   const int kh = ((o[O_K] + 7) & ~7) / 2, act = o[O_EACT], act2 = o[O_AUX2];
-  return o[O_EDROP] >= 0 ? pick_d<true>(kh, act, act2, o[O_MODE]) : pick_d<false>(kh, act, act2, o[O_MODE]);
+  if (split)
+    return o[O_EDROP] >= 0 ? pick_d<true, true>(kh, act, act2, o[O_MODE]) : pick_d<false, true>(kh, act, act2, o[O_MODE]);
+  return o[O_EDROP] >= 0 ? pick_d<true, false>(kh, act, act2, o[O_MODE]) : pick_d<false, false>(kh, act, act2, o[O_MODE]);
 }
 
 static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int& act, int& drop) {
@@ -504,27 +586,44 @@ int mlp2_supported(const int* w) {
          o[O_AUX3] == 3 && (o[O_K] & 3) == 0 && o[O_K] <= 96 && lds <= 160 * 1024;
 }
 
-int mlp2_grid_cap(const int* w, int n_cu) {
-  int kh, rbw, ncb, lds, act, drop;
-  geom(w, kh, rbw, ncb, lds, act, drop);
+static int per_cu_of(mlp2_fn k, int ncb, int lds) {
   hipFuncAttributes attr;
   int per_cu = 1;
-  if (hipFuncGetAttributes(&attr, (const void*)pick(w)) == hipSuccess) {
+  if (hipFuncGetAttributes(&attr, (const void*)k) == hipSuccess) {
     const int vg = ((attr.numRegs + 7) / 8) * 8;
     const int waves_simd = vg > 0 ? (512 / vg > 8 ? 8 : 512 / vg) : 8;
     per_cu = (4 * waves_simd) / ncb;
   }
   const int by_lds = (160 * 1024) / lds;
   if (per_cu > by_lds) per_cu = by_lds;
-  if (per_cu < 1) per_cu = 1;
-  return n_cu * per_cu;
+  return per_cu < 1 ? 1 : per_cu;
 }
 
-int mlp2_launch(const int* w, const Args& a, int grid, hipStream_t s) {
+// one grid for both instantiations (the exact one recomputes a flagged split launch into the same
+// per-workgroup slabs): the smaller of their occupancies
+int mlp2_grid_cap(const int* w, int n_cu) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
-  mlp2_fn k = pick(w);
+  const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds);
+  return n_cu * (a < b ? a : b);
+}
+
+static int launch_k(mlp2_fn k, int ncb, int lds, const Args& a, int grid, hipStream_t s) {
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   hipLaunchKernelGGL(k, dim3(grid), dim3(ncb * 64), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// split instantiation, then the exact one, which exits at once unless the split launch flagged a
+// non-finite value (guard == epoch); hpe_set_exact_fp32(1): the exact kernel alone
+int mlp2_launch(const int* w, const Args& a, int grid, hipStream_t s) {
+  int kh, rbw, ncb, lds, act, drop;
+  geom(w, kh, rbw, ncb, lds, act, drop);
+  if (hpe_exact_fp32() || !a.guard) {
+    Args e = a;
+    e.guard = nullptr;
+    return launch_k(pick(w), ncb, lds, e, grid, s);
+  }
+  if (launch_k(pick(w, true), ncb, lds, a, grid, s)) return 2;
+  return launch_k(pick(w), ncb, lds, a, grid, s);
 }
