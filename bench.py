@@ -34,7 +34,18 @@ C = 96
 PER_GPU = 512
 INFER_B = 256
 PEAK_FP32 = 157.3e12      # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
+PEAK_F16 = 2.5e15         # MI355X dense FP16 MFMA (no sparsity), MI355X_MICROARCH.md
 PEAK_HBM = 8.0e12
+
+
+def gemm_peak():
+    """The MFMA ceiling of the regressor GEMMs as libhpe.so runs them: by default every fp32 product is
+    three fp16 MFMA products (hi/lo split, fp32 accumulate; csrc/hpe_common.h mfma3), so the
+    fp32-equivalent ceiling is the dense fp16 peak / 3; HPE_EXACT_FP32=1 selects the exact fp32 MFMA."""
+    if os.environ.get('HPE_EXACT_FP32') == '1':
+        return PEAK_FP32, 'exact fp32 MFMA (v_mfma_f32_32x32x2_f32), peak = dense fp32'
+    return PEAK_F16 / 3, ('fp32 GEMMs as 3 fp16 MFMA products (hi/lo split, fp32 accumulate); '
+                          'peak = 2.5 PFLOP/s dense fp16 / 3, in fp32-equivalent FLOP/s')
 # algorithmic work per position (SURVEY.md §8d): 2*MAC of conv layers only
 TRAIN_FLOP_POS = 2 * (C * F + F * 3) * 2 + 2 * F * 3      # fwd + dW + dX(layer 2) = 144,720
 INFER_FLOP_POS = 2 * (96 * 32 + 32 * 16 + 16 * 3)         # hrchr82r: 7,264
@@ -144,8 +155,9 @@ def bench_train88(hpe, keras, dev, steps, warmup):
                         '512 images of 88x88 feature maps',
             'value': n / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3, 'dtype': 'fp32',
             'kernel': eng.program('train', Pm).prog.kind + '_kernel + reduce_kernel',
-            'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': PEAK_FP32 / 1e12, 'unit': 'TFLOP/s',
-                         'frac': ach / PEAK_FP32, 'traffic': _traffic('train88'), 'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
+            'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': gemm_peak()[0] / 1e12, 'unit': 'TFLOP/s',
+                         'frac': ach / gemm_peak()[0], 'gemm': gemm_peak()[1], 'traffic': _traffic('train88'),
+                         'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
 
 
 BLAZE_B = 1024
@@ -323,8 +335,8 @@ def main():
                                    '(configs[3] per GPU)',
                        'global_batch': n_global, 'positions_per_image': P, 'channels': C,
                        'parallelism': 'dp%d' % world},
-            'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': PEAK_FP32 / 1e12,
-                         'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32,
+            'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': gemm_peak()[0] / 1e12,
+                         'unit': 'TFLOP/s', 'frac': achieved / gemm_peak()[0], 'gemm': gemm_peak()[1],
                          'traffic': _traffic('train'),
                          'kernel': {'mlp2': 'mlp2_kernel', 'generic': 'rowprog_kernel'}.get(
                              eng.program('train', P).prog.kind, '?') + ' + reduce_kernel (hpe_train_step + hpe_reduce)',
@@ -367,7 +379,7 @@ def main():
                          'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
                          'frac': bytes_launch / (ims * 1e-3) / PEAK_HBM,
                          'traffic': _traffic('infer'),
-                         'kernel': {'chain': 'chain_fwd_kernel', 'generic': 'rowprog_kernel'}.get(
+                         'kernel': {'chain': 'chain_split_kernel (+ guarded chain_fwd_kernel)', 'generic': 'rowprog_kernel'}.get(
                              ie.program('fwd', P).prog.kind, '?') + ' (hpe_forward)',
                          'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
                          'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}

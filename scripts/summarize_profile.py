@@ -51,13 +51,16 @@ def main(tag):
         fb, wb, _ = per[short]
         res[key] = {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb, 'hbm_bytes_per_launch': fb + wb}
 
-    # bench lines -> their dominant kernels (template args: <KH, ACT1, DROP, NWM>; ACT 1 = tanh, 3 = softsign)
+    # bench lines -> their dominant kernels (template args: <KH, ACT1, DROP, NWM, SPLIT>; ACT 1 = tanh,
+    # 3 = softsign).  The exact-fp32 instantiations (SPLIT false) are the guarded fallbacks that exit
+    # at once unless the split launch flagged an overflow; the split ones carry the traffic.
+    split = os.environ.get('HPE_EXACT_FP32') != '1'
     for short in per:
-        if short.startswith('void mlp2_kernel<48') and ', false' in short:
+        if short.startswith('void mlp2_kernel<48') and ', 1, false, 12, %s>' % str(split).lower() in short:
             put('train', short)
-        elif short.startswith('void mlp2_kernel<44') and ', true' in short:
+        elif short.startswith('void mlp2_kernel<44') and ', true, 4, %s>' % str(split).lower() in short:
             put('train88', short)
-        elif 'chain_fwd' in short:
+        elif ('chain_split' if split else 'chain_fwd') in short:
             put('infer', short)
     # BlazeFace forward = every bf_* launch of one forward (one dispatch each per forward per kernel
     # name, except the 64x64/32x32 block kernels that run several blocks): bytes per forward

@@ -198,3 +198,51 @@ def test_chain_split_precision_and_overflow_guard():
     np.testing.assert_allclose(got, refo, rtol=RTOL, atol=ATOL)
     # the next launch (new epoch) is back on the split path and still right
     np.testing.assert_allclose(eng.forward(xt, 1).cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize('rid', ['sqnu665j', 'stoqa9pt'])
+def test_train_step_split_vs_exact_and_guard(rid):
+    """The fused training step's fp16-split GEMMs (csrc/hpe_mlp2.hip SPLIT) against its exact-fp32
+    instantiation and the float64 oracle's gradient, on 96x96 / 88x88-sized row counts; a feature
+    outside the fp16 range makes the split launch hand the step to the exact one (guard word)."""
+    from hpe import _lib
+    from hpe.engine import Engine
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    eng = Engine(mc, w)
+    assert eng.program('train', 1).prog.kind == 'mlp2'
+    n = 3000
+    x = features(n, c, seed=21)
+    y = labels(n, seed=22)
+    xt = torch.from_numpy(x.reshape(n, c)).cuda()
+    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
+    inv = 1.0 / (n * 3)
+
+    def grad(xd):
+        return eng.gradient(xd, yt, 1, None, n, inv, seed=5).cpu().numpy().copy()
+
+    lib = _lib.load()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        g_exact = grad(xt)
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    g_split = grad(xt)
+    npt = eng.n_train
+    scale = np.abs(g_exact[:npt]).max()
+    d = np.abs(g_split[:npt] - g_exact[:npt]).max() / scale
+    print('%s: max |split - exact| / max |g| = %.2e' % (rid, d))
+    assert d < 2e-5, d
+    np.testing.assert_allclose(g_split[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
+    # guard: one feature at 1e5 -> the split launch flags, the exact instantiation recomputes
+    xo = x.reshape(n, c).copy()
+    xo[17, 5] = 1.0e5
+    xot = torch.from_numpy(xo).cuda()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        go_exact = grad(xot)
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    go = grad(xot)
+    assert np.isfinite(go).all()
+    np.testing.assert_array_equal(go, go_exact)
