@@ -25,6 +25,10 @@
 #define MLP2_XS 100             // LDS row stride of an X tile (floats): conflict-free, 16-B aligned
 #define MLP2_XF (32 * MLP2_XS)  // floats per X tile buffer
 #define MLP2_LAB 128            // floats per label buffer: [32 rows][4] (yaw, pitch, roll, pad)
+// pre-split X tiles (SPLIT kernels of the 12-wave variant, see presplit_tile): fp16 hi / lo halves
+#define MLP2_FS 104             // row stride (halves) of the forward layout [32 rows][2 x 48]: conflict-free b128
+#define MLP2_TS 40              // row stride (halves) of the transposed layout [96 channels][32 rows]
+#define MLP2_PRE_HALVES (2 * 32 * MLP2_FS + 4 * 96 * MLP2_TS)  // fwd hi, lo + 2 parities x transposed hi, lo
 
 // LDS-DMA (global_load_lds) in inline asm: hipcc's waitcnt pass cannot tell the two X buffers
 // apart and would put vmcnt(0) before every ds_read of the tile in use, draining the prefetch of
@@ -162,6 +166,39 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
   }
 }
 
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+// One split of the landed X tile per workgroup instead of one per wave (the 12 waves all read the
+// whole tile, in two layouts): every thread turns 4 floats into fp16 hi / lo halves, written
+//   * forward layout  xf[r][48 h + m] = X[r][KH h + m] (zero for m >= KH): lane (row r, half h)
+//     reads K-step s as one b128 at 48 h + 8 s;
+//   * transposed      xt[k][p(r)] = X[r][k], p(r) = r with bits 2 and 3 swapped, so the 8 rows
+//     16 s + 8 (j >> 2) + 4 h + (j & 3) of the dW1 K-step s are the contiguous p = 16 s + 8 h + j:
+//     one b128 per (K-step, 32-channel block) instead of 8 strided b32 reads + a split per wave.
+// Pad channels [C_in, 96) of the raw tile hold zeros, so their xt rows are zero.
+template <int KH>
+__device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xfh, _Float16* xfl, _Float16* xth,
+                                              _Float16* xtl, int tid, int NT) {
+  for (int i = tid; i < 32 * 24; i += NT) {
+    const int r = i / 24, rem = i - r * 24, h = rem >= 12 ? 1 : 0, m0 = 4 * (rem - 12 * h);
+    const f32x4 v = m0 < KH ? *(const f32x4*)(xs + r * MLP2_XS + KH * h + m0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const h4 hi = __builtin_convertvector(v, h4);
+    const h4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), h4);
+    *(h4*)(xfh + r * MLP2_FS + 48 * h + m0) = hi;
+    *(h4*)(xfl + r * MLP2_FS + 48 * h + m0) = lo;
+  }
+  for (int i = tid; i < 96 * 8; i += NT) {
+    const int rg = i / 96, k = i - rg * 96, r = 4 * rg;
+    const f32x4 v = {xs[r * MLP2_XS + k], xs[(r + 1) * MLP2_XS + k], xs[(r + 2) * MLP2_XS + k],
+                     xs[(r + 3) * MLP2_XS + k]};
+    const int p = (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);
+    const h4 hi = __builtin_convertvector(v, h4);
+    const h4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), h4);
+    *(h4*)(xth + k * MLP2_TS + p) = hi;
+    *(h4*)(xtl + k * MLP2_TS + p) = lo;
+  }
+}
+
 // NWM: launch bound in waves (12: any width <= 384, 168-VGPR budget; 4: F <= 128, 256 budget)
 // SPLIT: both GEMMs on fp16 MFMA at fp32 accuracy (split8 / mfma3, hpe_common.h), same registers:
 //   forward  Z1 = X.W1: 6 K-steps of three v_mfma_f32_32x32x16_f16 (576 MFMA cycles per wave per
@@ -181,6 +218,11 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NKB = (2 * KH + 31) / 32;  // 32-row blocks of dW1 (input channels)
   constexpr int T = 32;
+  // PRE: the split kernel of the 12-wave variant splits each X tile once per workgroup
+  // (presplit_tile) after it lands, one tile ahead, after the head phase's barrier; the raw tile
+  // buffer is then single (consumed by the split before the barrier that opens its tile)
+  constexpr bool PRE = SPLIT && NWM == MLP2_MAXW;
+  constexpr int NXB = PRE ? 1 : 2;
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int mode = prog[H_MODE];
@@ -193,7 +235,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   const bool nok = n < F;
   // LDS: X tiles [2][32][MLP2_XS] | labels [2][128] | head partials [NCB][T][4] | dZ2 [T][4] | scratch
   float* xbuf = lds;
-  float* lbuf = xbuf + 2 * MLP2_XF;
+  float* lbuf = xbuf + NXB * MLP2_XF;
   float* part = lbuf + 2 * MLP2_LAB;
   float* dz2 = part + NCB * T * 4;
   float* a1s = dz2 + T * 4;       // [NCB][16][64]: layer-1 activations, forward -> backward
@@ -201,6 +243,9 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
   float* red = hacc + NCB * 256;  // [NCB * 64]
+  _Float16* xfh = (_Float16*)(red + NCB * 64);  // PRE: [32][MLP2_FS] hi, lo; [2][96][MLP2_TS] hi, lo
+  _Float16* xfl = xfh + 32 * MLP2_FS;
+  _Float16* xtb = xfl + 32 * MLP2_FS;
 
   E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
   E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
@@ -257,7 +302,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 
   // pad columns [C_in, 96) of both X buffers: never written by the staging, read by the forward
   // MFMA against zero weights -> must hold zeros, not stale LDS
-  for (int i = threadIdx.x; i < 64 * 16; i += NT) {
+  for (int i = threadIdx.x; i < NXB * 32 * 16; i += NT) {
     const int r = i >> 4, c = Cin + (i & 15);
     if (c < 96) xbuf[r * MLP2_XS + c] = 0.f;
   }
@@ -269,19 +314,25 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   ti.img0 = (int)(blockIdx.x * T / P);
   ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
   if (blockIdx.x < ntiles) stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, ti, wave, NCB, lane, Cin, labels);
+  if constexpr (PRE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar_lds();
+    presplit_tile<KH>(xbuf, xfh, xfl, xtb, xtb + 96 * MLP2_TS, threadIdx.x, NT);
+  }
   int buf = 0;
   for (int tile = blockIdx.x; tile < (int)ntiles; tile += gridDim.x, buf ^= 1, ti.advance(dq, dr)) {
     const int64_t row0 = (int64_t)tile * T;
-    const float* xs = xbuf + buf * MLP2_XF;
+    const float* xs = xbuf + (PRE ? 0 : buf) * MLP2_XF;
     const float* lab = lbuf + buf * MLP2_LAB;
     // tile `tile` landed (own pieces) -> barrier: every wave's pieces landed, and every wave is
-    // done with tile - gridDim.x, whose buffer the prefetch below overwrites
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // done with tile - gridDim.x, whose buffer the prefetch below overwrites (PRE: the tile was
+    // split before this barrier, the raw buffer is free)
+    if constexpr (!PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar_lds();
     if (tile + gridDim.x < ntiles) {
       TileImg tn = ti;
       tn.advance(dq, dr);
-      stage_tile(args, xbuf + (buf ^ 1) * MLP2_XF, lbuf + (buf ^ 1) * MLP2_LAB,
+      stage_tile(args, xbuf + (PRE ? 0 : (buf ^ 1)) * MLP2_XF, lbuf + (buf ^ 1) * MLP2_LAB,
                  (int64_t)(tile + gridDim.x) * T, tn, wave, NCB, lane, Cin, labels);
     }
 
@@ -290,7 +341,16 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     {
       const float* ap = xs + l32 * MLP2_XS + half * KH;
       f32x16 acc = {};
-      if constexpr (SPLIT) {
+      if constexpr (PRE) {
+        const _Float16* fh = xfh + l32 * MLP2_FS + 48 * half;
+        const _Float16* fl = xfl + l32 * MLP2_FS + 48 * half;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+          acc = mfma3(*(const h8*)(fh + 8 * s), *(const h8*)(fl + 8 * s), wh[s], wl[s], acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
+      } else if constexpr (SPLIT) {
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
           const f32x4 a0 = *(const f32x4*)(ap + 8 * s), a1 = *(const f32x4*)(ap + 8 * s + 4);
@@ -404,8 +464,20 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
         }
       }
     }
-    if (!train) continue;  // the next tile's first barrier orders part / lab reuse
-    bar_lds();
+    if constexpr (PRE) {
+      // the next tile landed -> barrier -> split it (forward layout: this tile's forward is done;
+      // transposed: the other parity, this tile's backward reads its own)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar_lds();
+      if (tile + gridDim.x < ntiles) {
+        _Float16* xt = xtb + (buf ^ 1) * 2 * 96 * MLP2_TS;
+        presplit_tile<KH>(xbuf, xfh, xfl, xt, xt + 96 * MLP2_TS, threadIdx.x, NT);
+      }
+      if (!train) continue;
+    } else {
+      if (!train) continue;  // the next tile's first barrier orders part / lab reuse
+      bar_lds();
+    }
 
     // ---- backward: dA1 = dZ2.W2^T, dZ1, dW2, db1 in registers; dW1 += X^T.dZ1 on MFMA ----
     {
@@ -443,6 +515,16 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
           }
           h8 dh, dl;
           split8(dv, dh, dl);
+          if constexpr (PRE) {
+            const _Float16* th = xtb + buf * 2 * 96 * MLP2_TS + l32 * MLP2_TS + 16 * s + 8 * half;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+              dw[kb] = mfma3(*(const h8*)(th + kb * 32 * MLP2_TS), *(const h8*)(th + (96 + kb * 32) * MLP2_TS),
+                             dh, dl, dw[kb]);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+          }
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) {
             const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
@@ -575,7 +657,11 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  lds_bytes = (2 * MLP2_XF + 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64) * 4;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64;
+  lds_bytes = (2 * MLP2_XF + rest) * 4;
+  // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
+  const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;
+  if (ncb > 4 && pre > lds_bytes) lds_bytes = pre;
 }
 
 int mlp2_supported(const int* w) {
