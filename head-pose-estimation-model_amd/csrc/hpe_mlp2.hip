@@ -320,6 +320,13 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     presplit_tile<KH>(xbuf, xfh, xfl, xtb, xtb + 96 * MLP2_TS, threadIdx.x, NT);
   }
   int buf = 0;
+#ifdef MLP2_STAMPS
+  uint32_t ph[9] = {};
+  uint64_t tprev = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[i] += (uint32_t)(t_ - tprev); tprev = t_; } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
   for (int tile = blockIdx.x; tile < (int)ntiles; tile += gridDim.x, buf ^= 1, ti.advance(dq, dr)) {
     const int64_t row0 = (int64_t)tile * T;
     const float* xs = xbuf + (PRE ? 0 : buf) * MLP2_XF;
@@ -328,7 +335,9 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     // done with tile - gridDim.x, whose buffer the prefetch below overwrites (PRE: the tile was
     // split before this barrier, the raw buffer is free)
     if constexpr (!PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(0);
     bar_lds();
+    STAMP(1);
     if (tile + gridDim.x < ntiles) {
       TileImg tn = ti;
       tn.advance(dq, dr);
@@ -336,6 +345,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
                  (int64_t)(tile + gridDim.x) * T, tn, wave, NCB, lane, Cin, labels);
     }
 
+    STAMP(2);
     // ---- forward: Z1 = X.W1 (+b1, act, dropout) and the head partials ----
     uint32_t dmask = 0;  // layer-1 dropout keep bits of this lane's 16 rows (reused by backward)
     {
@@ -350,6 +360,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
           __builtin_amdgcn_sched_barrier(0);
         }
         bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
+        STAMP(3);
       } else if constexpr (SPLIT) {
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
@@ -428,7 +439,9 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
         if (half == 0) *(f32x4*)(part + (wave * T + r) * 4) = f32x4{s0, s1, s2, 0.f};
       }
     }
+    STAMP(4);
     bar_lds();
+    STAMP(5);
 
     // ---- head: sum partials (fixed wave order) + b2, epilogue, loss / output ----
     for (int it = threadIdx.x; it < T * 3 && threadIdx.x < NT3; it += NT3) {
@@ -464,11 +477,13 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
         }
       }
     }
+    STAMP(6);
     if constexpr (PRE) {
       // the next tile landed -> barrier -> split it (forward layout: this tile's forward is done;
       // transposed: the other parity, this tile's backward reads its own)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar_lds();
+      STAMP(7);
       if (tile + gridDim.x < ntiles) {
         _Float16* xt = xtb + (buf ^ 1) * 2 * 96 * MLP2_TS;
         presplit_tile<KH>(xbuf, xfh, xfl, xt, xt + 96 * MLP2_TS, threadIdx.x, NT);
@@ -479,6 +494,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       bar_lds();
     }
 
+    STAMP(8);
     // ---- backward: dA1 = dZ2.W2^T, dZ1, dW2, db1 in registers; dW1 += X^T.dZ1 on MFMA ----
     {
       const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
@@ -502,7 +518,30 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
         db1 += gz;
         return gz;
       };
-      if constexpr (SPLIT) {
+      if constexpr (PRE) {
+        // dZ1 of K-step 0 -> split -> its 9 MFMAs, with the VALU of K-step 1's dZ1 free to issue
+        // under them (no scheduling fences between the two), then K-step 1's MFMAs
+        const _Float16* th = xtb + buf * 2 * 96 * MLP2_TS + l32 * MLP2_TS + 8 * half;
+        f32x8 dv0, dv1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv0[j] = dz_of(j);
+        h8 d0h, d0l;
+        split8(dv0, d0h, d0l);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+          dw[kb] = mfma3(*(const h8*)(th + kb * 32 * MLP2_TS), *(const h8*)(th + (96 + kb * 32) * MLP2_TS),
+                         d0h, d0l, dw[kb]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv1[j] = dz_of(8 + j);
+        __builtin_amdgcn_sched_barrier(0);
+        h8 d1h, d1l;
+        split8(dv1, d1h, d1l);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+          dw[kb] = mfma3(*(const h8*)(th + 16 + kb * 32 * MLP2_TS), *(const h8*)(th + 16 + (96 + kb * 32) * MLP2_TS),
+                         d1h, d1l, dw[kb]);
+      } else if constexpr (SPLIT) {
         // K-step s (rows 16 s + 8 (j >> 2) + 4 h + (j & 3)): dZ1 registers 8 s .. 8 s + 7 as the B
         // operand, the matching X^T rows as A; one K-step at a time keeps the live set small
 #pragma unroll
@@ -515,16 +554,6 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
           }
           h8 dh, dl;
           split8(dv, dh, dl);
-          if constexpr (PRE) {
-            const _Float16* th = xtb + buf * 2 * 96 * MLP2_TS + l32 * MLP2_TS + 16 * s + 8 * half;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-              dw[kb] = mfma3(*(const h8*)(th + kb * 32 * MLP2_TS), *(const h8*)(th + (96 + kb * 32) * MLP2_TS),
-                             dh, dl, dw[kb]);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-            continue;
-          }
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) {
             const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
@@ -565,6 +594,11 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     }
   }
 
+#ifdef MLP2_STAMPS
+  if (PRE && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 5))
+    printf("STAMP w%d bwd+tail %u bar1 %u stage %u fwdmfma %u act+part %u bar2 %u head %u bar3 %u presplit %u\n", wave,
+           ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
+#endif
   if (mode == MODE_FWD) {
     if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
