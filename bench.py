@@ -9,15 +9,27 @@ forward+loss+backward kernel, the workgroup-partial reduce, one RCCL all-reduce 
 gradient when N > 1, and the fused Adam kernel — exactly one ``fit`` step of the reference.
 Inputs are resident in HBM before the timed region.
 
-Also reported: ``infer`` (configs[1]: the selected Model-96 head hrchr82r, batch 256 on 96x96
-maps, forward only) and ``cpu_baseline`` (the oracle's torch-CPU fp32 restatement of the same
-training step on a bounded sample, rank 0, N=1 only).
+Also reported (sub-objects of the one JSON line):
+  strong     configs[3] as written: global batch 4096 images split over the N ranks (strong scaling)
+  p1         the reference's own regime (train_96.py:134-140,175-183): 1x1 maps (P = 1), batch 128
+             and 512, through Model.fit (per-step launches vs the fused epoch kernel), per-step us,
+             with the CPU restatement timed at the same batch
+  infer      configs[1]: the selected Model-96 head hrchr82r, batch 256 on 96x96 maps, forward only
+  train88    Model-88 create_model on 88x88 maps
+  blazeface  configs[4]: unified BlazeFace + both pose heads, batch 1024
+  cpu_baseline  the oracle's torch-CPU fp32 restatement of the headline step on a bounded sample
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (N>1: torchrun, one rank per GPU)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1 without a torchrun environment: this process starts
+  ``python -m torch.distributed.run --nproc-per-node N ... bench.py`` as a CHILD (before anything
+  touches the GPU) and exits with its code; under torchrun (RANK / WORLD_SIZE set) it is one rank.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,6 +44,7 @@ F = 360
 H = W = 96
 C = 96
 PER_GPU = 512
+STRONG_GLOBAL = 4096
 INFER_B = 256
 PEAK_FP32 = 157.3e12      # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
 PEAK_F16 = 2.5e15         # MI355X dense FP16 MFMA (no sparsity), MI355X_MICROARCH.md
@@ -46,36 +59,136 @@ def gemm_peak():
         return PEAK_FP32, 'exact fp32 MFMA (v_mfma_f32_32x32x2_f32), peak = dense fp32'
     return PEAK_F16 / 3, ('fp32 GEMMs as 3 fp16 MFMA products (hi/lo split, fp32 accumulate); '
                           'peak = 2.5 PFLOP/s dense fp16 / 3, in fp32-equivalent FLOP/s')
+
+
 # algorithmic work per position: 2*MAC of conv layers only
 TRAIN_FLOP_POS = 2 * (C * F + F * 3) * 2 + 2 * F * 3      # fwd + dW + dX(layer 2) = 144,720
 INFER_FLOP_POS = 2 * (96 * 32 + 32 * 16 + 16 * 3)         # hrchr82r: 7,264
 INFER_BYTES_POS = 4 * 96 + 4 * 3                          # fp32 in + fp32 out
 
 
-def build_train_model(hpe, keras):
-    """create_model() of Model-96/train_96.py:65-110 with num_filters=360, dropout 0, l2 0.1."""
-    reg = keras.regularizers.l2(0.1)
+# ---------------------------------------------------------------------------------------------
+# N-rank launch (no GPU call before this decision)
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_plan(gpus, argv, env):
+    """Command line of the N-rank child launch, or None when this process is itself the job
+    (N == 1, or already a torchrun rank).  Pure: touches no device."""
+    if gpus <= 1 or 'WORLD_SIZE' in env:
+        return None
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(gpus),
+            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(gpus, argv):
+    """Run ``gpus`` ranks as a child torchrun job; returns its exit code.  Counting devices with
+    torch.cuda.device_count() does not initialise the GPU on this image."""
+    n_dev = torch.cuda.device_count()
+    if n_dev < gpus:
+        print('bench.py: --gpus %d requested but only %d GPU(s) visible' % (gpus, n_dev), file=sys.stderr)
+        return 2
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(launch_plan(gpus, argv, {}), env=env)
+
+
+# ---------------------------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------------------------
+def build_train_model(keras, F_=F, l2=0.1, dropout=0.0):
+    """create_model() of Model-96/train_96.py:65-110 with num_filters=F_, dropout, l2."""
+    reg = keras.regularizers.l2(l2)
     inp = keras.Input(shape=(None, None, 96))
-    x1 = keras.layers.Conv2D(filters=F, kernel_size=1, padding='same', activation='tanh',
+    x1 = keras.layers.Conv2D(filters=F_, kernel_size=1, padding='same', activation='tanh',
                              kernel_initializer=keras.initializers.GlorotUniform(),
                              bias_regularizer=reg, kernel_regularizer=reg)(inp)
-    x1 = keras.layers.SpatialDropout2D(0.0)(x1)
+    x1 = keras.layers.SpatialDropout2D(dropout)(x1)
     out = keras.layers.Conv2D(filters=3, kernel_size=1, padding='same', activation=None,
                               kernel_initializer=keras.initializers.GlorotUniform(),
                               bias_regularizer=reg, kernel_regularizer=reg)(x1)
-    out = keras.layers.SpatialDropout2D(0.0)(out)
+    out = keras.layers.SpatialDropout2D(dropout)(out)
     m = keras.Model(inputs=inp, outputs=out)
     m.compile(optimizer=keras.optimizers.Adam(learning_rate=0.00028), loss='mse', metrics=['mae'])
     return m
 
 
-def synth(n_img, seed, device):
+def synth(n_img, seed, device, P=H * W, c=C):
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    x = torch.randn((n_img * H * W, C), generator=g, device=device, dtype=torch.float32)
+    x = torch.randn((n_img * P, c), generator=g, device=device, dtype=torch.float32)
     x = torch.clamp_min(0.6 * x - 0.3, 0.0)
     y = 20.0 * torch.randn((n_img, 3), generator=g, device=device, dtype=torch.float32)
     return x.contiguous(), y.contiguous()
+
+
+def run_train(eng, opt, x, y, P, n_local, n_global, rank, world, steps, warmup, dist):
+    """Timed training steps (barrier + synchronize on both sides, max over ranks).  Returns
+    (seconds, mean ms of the train_step + reduce launches measured with HIP events on the launch
+    stream, mse of the last step)."""
+    inv_count = 1.0 / (n_global * P * 3)
+    stats = torch.zeros((steps + warmup + 1, 2 + eng.optim_grid()), device=x.device)
+    for i in range(warmup):
+        eng.gradient(x, y, P, None, n_local, inv_count, seed=i + 1, img_off=rank * n_local)
+        if dist is not None:
+            dist.all_reduce(eng.grad)
+        eng.optimizer_step(opt, stats[i])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    marks = []
+    for i in range(steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        eng.gradient(x, y, P, None, n_local, inv_count, seed=warmup + i + 1, img_off=rank * n_local)
+        e1.record()
+        marks.append((e0, e1))
+        if dist is not None:
+            dist.all_reduce(eng.grad)
+        eng.optimizer_step(opt, stats[warmup + i])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=x.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in marks]))
+    mse = float(stats[warmup + steps - 1, 0].item()) / (n_global * P * 3)
+    return dt, kms, mse
+
+
+def _threads_for_cpu(probe):
+    """Thread count for the CPU restatement: every CPU this process may run on
+    (os.sched_getaffinity), unless the box's OMP_NUM_THREADS share runs the probe faster (an
+    oversubscribed cgroup quota).  Returns (threads, {threads: probe seconds})."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    cands = sorted({allowed, int(os.environ.get('OMP_NUM_THREADS', allowed) or allowed)})
+    times = {}
+    for t in cands:
+        torch.set_num_threads(t)
+        probe()
+        t0 = time.perf_counter()
+        probe()
+        times[t] = time.perf_counter() - t0
+    best = min(times, key=times.get)
+    torch.set_num_threads(best)
+    return best, times
 
 
 def cpu_baseline(weights_cfg, steps_budget_s=12.0):
@@ -84,8 +197,6 @@ def cpu_baseline(weights_cfg, steps_budget_s=12.0):
     ~steps_budget_s."""
     sys.path.insert(0, ROOT)
     from oracle import keras_ref as K
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     mc, w = weights_cfg
     g = K.Graph(mc, w, dtype=torch.float32)
     opt = K.LegacyOptimizer('adam', 2.8e-4)
@@ -94,7 +205,7 @@ def cpu_baseline(weights_cfg, steps_budget_s=12.0):
     x = np.maximum(0.0, 0.6 * rng.standard_normal((n, H, W, C)) - 0.3).astype(np.float32)
     y = (20 * rng.standard_normal((n, 3))).astype(np.float32)
     xt, yt = torch.from_numpy(x), torch.from_numpy(y)
-    K.train_step(g, opt, xt, yt)  # warm-up
+    threads, probes = _threads_for_cpu(lambda: K.train_step(g, opt, xt, yt))
     t0 = time.perf_counter()
     steps = 0
     while time.perf_counter() - t0 < steps_budget_s or steps < 2:
@@ -104,7 +215,100 @@ def cpu_baseline(weights_cfg, steps_budget_s=12.0):
     return {'value': steps * n / dt, 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
             'sample': '%d training steps x %d images of 96x96x96 (create_model(360), Adam, '
                       'torch-CPU fp32 restatement, oracle/keras_ref.py), %.1f s' % (steps, n, dt),
-            'cpu': _cpu_name()}
+            'cpu': _cpu_name(), 'os_cpu_count': os.cpu_count(),
+            'thread_probe_s': {str(k): round(v, 4) for k, v in probes.items()}}
+
+
+class _EpochTimer:
+    """keras-style callback: wall time of every epoch of fit (per-epoch host work included)."""
+
+    def __init__(self):
+        self.model = None
+        self.params = {}
+        self.times = []
+
+    def set_model(self, m):
+        self.model = m
+
+    def set_params(self, p):
+        self.params = p
+
+    def on_train_begin(self, logs=None):
+        pass
+
+    def on_train_end(self, logs=None):
+        pass
+
+    def on_epoch_begin(self, epoch, logs=None):
+        self.t0 = time.perf_counter()
+
+    def on_epoch_end(self, epoch, logs=None):
+        self.times.append(time.perf_counter() - self.t0)
+
+
+def bench_p1(keras, batches=(128, 512), n_rows=1 << 20, epochs=3, no_cpu=False):
+    """The reference's training regime (train_96.py:134-140,175-183): create_model(360), Adam,
+    1x1 feature maps (P = 1), 80/20 split with validation each epoch, batch 128 (the reference's)
+    and 512, through Model.fit.  Per-step time = median epoch wall time / steps per epoch, for the
+    per-step launch path (train_step + reduce + optimizer launches per step, HPE_FIT_FUSED=0) and
+    the fused epoch kernel (one launch per epoch; default)."""
+    import hpe
+    from hpe.data import train_test_split
+    rng = np.random.default_rng(0)
+    x = np.maximum(0.0, 0.6 * rng.standard_normal((n_rows, 1, 1, C)) - 0.3).astype(np.float32)
+    y = (20 * rng.standard_normal((n_rows, 1, 1, 3))).astype(np.float32)
+    tx, vx, ty, vy = train_test_split(x, y, test_size=0.2, random_state=42)
+    out = {'workload': 'Model-96 create_model(360, dropout 0, l2 0.1), legacy Adam, synthetic 1x1x96 '
+                       'features, %d rows (80/20 split, validation every epoch), Model.fit' % n_rows,
+           'unit': 'us/step', 'lines': {}}
+    prev = os.environ.get('HPE_FIT_FUSED')
+    try:
+        for bs in batches:
+            steps = math.ceil(tx.shape[0] / bs)
+            for mode in ('per_step', 'fused_epoch'):
+                os.environ['HPE_FIT_FUSED'] = '0' if mode == 'per_step' else '1'
+                hpe.set_seed(42)
+                keras.backend.clear_session()
+                m = build_train_model(keras)
+                tm = _EpochTimer()
+                ep = 1 if mode == 'per_step' and bs <= 128 else epochs
+                m.fit(tx, ty, batch_size=bs, epochs=ep + 1, validation_data=(vx, vy), callbacks=[tm],
+                      verbose=0)
+                t_ep = float(np.median(tm.times[1:]))
+                out['lines']['%s_b%d' % (mode, bs)] = {
+                    'us_per_step': t_ep / steps * 1e6, 'images_per_sec': tx.shape[0] / t_ep,
+                    'epoch_s': t_ep, 'steps_per_epoch': steps, 'epochs_timed': len(tm.times) - 1,
+                    'fused': bool(getattr(m, '_last_fit_fused', False)),
+                    'final_loss': float(m.history.history['loss'][-1])}
+            ps, fe = out['lines']['per_step_b%d' % bs], out['lines']['fused_epoch_b%d' % bs]
+            out['lines']['speedup_b%d' % bs] = ps['us_per_step'] / fe['us_per_step']
+    finally:
+        if prev is None:
+            os.environ.pop('HPE_FIT_FUSED', None)
+        else:
+            os.environ['HPE_FIT_FUSED'] = prev
+    if not no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import keras_ref as K
+        keras.backend.clear_session()
+        m = build_train_model(keras)
+        g = K.Graph(m.model_config, m.weights_dict(), dtype=torch.float32)
+        opt = K.LegacyOptimizer('adam', 2.8e-4)
+        res = {}
+        for bs in batches:
+            xb, yb = torch.from_numpy(tx[:bs]), torch.from_numpy(ty[:bs].reshape(bs, 3))
+            threads, _ = _threads_for_cpu(lambda: K.train_step(g, opt, xb, yb))
+            t0 = time.perf_counter()
+            k = 0
+            while time.perf_counter() - t0 < 4.0 or k < 5:
+                K.train_step(g, opt, xb, yb)
+                k += 1
+            dt = (time.perf_counter() - t0) / k
+            res['b%d' % bs] = {'us_per_step': dt * 1e6, 'images_per_sec': bs / dt, 'cores': threads,
+                               'kind': 'port', 'sample': '%d steps of batch %d (oracle/keras_ref.py '
+                                                         'torch-CPU fp32)' % (k, bs)}
+        out['cpu_baseline'] = res
+    return out
 
 
 def bench_train88(hpe, keras, dev, steps, warmup):
@@ -124,36 +328,13 @@ def bench_train88(hpe, keras, dev, steps, warmup):
     m.compile(optimizer=keras.optimizers.Adam(learning_rate=0.00028), loss='mse', metrics=['mae'])
     eng = m._eng()
     n, Pm = PER_GPU, 88 * 88
-    g = torch.Generator(device=dev)
-    g.manual_seed(88)
-    x = torch.clamp_min(0.6 * torch.randn((n * Pm, 88), generator=g, device=dev) - 0.3, 0.0).contiguous()
-    y = (20.0 * torch.randn((n, 3), generator=g, device=dev)).contiguous()
-    inv = 1.0 / (n * Pm * 3)
-    stats = torch.zeros((steps + warmup + 1, 2 + eng.optim_grid()), device=dev)
-    for i in range(warmup):
-        eng.gradient(x, y, Pm, None, n, inv, seed=i + 1)
-        eng.optimizer_step(m.optimizer, stats[i])
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    ks = []
-    t0 = time.perf_counter()
-    for i in range(steps):
-        a0 = torch.cuda.Event(enable_timing=True)
-        a1 = torch.cuda.Event(enable_timing=True)
-        a0.record()
-        eng.gradient(x, y, Pm, None, n, inv, seed=warmup + i + 1)
-        a1.record()
-        ks.append((a0, a1))
-        eng.optimizer_step(m.optimizer, stats[warmup + i])
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    kms = float(np.mean([a.elapsed_time(b) for a, b in ks]))
+    x, y = synth(n, 88, dev, P=Pm, c=88)
+    dt, kms, _ = run_train(eng, m.optimizer, x, y, Pm, n, n, 0, 1, steps, warmup, None)
     flop = 2 * (88 * 64 + 64 * 3) * 2 + 2 * 64 * 3            # fwd + dW + dX(layer 2) per position
     ach = flop * n * Pm / (kms * 1e-3)
     return {'workload': 'Model-88 create_model (88-64 softsign-3, dropout 1e-4, l2 1e-6) training, legacy Adam, '
                         '512 images of 88x88 feature maps',
-            'value': n / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3, 'dtype': 'fp32',
+            'value': n * steps / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3 / steps, 'dtype': 'fp32',
             'kernel': eng.program('train', Pm).prog.kind + '_kernel + reduce_kernel',
             'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': gemm_peak()[0] / 1e12, 'unit': 'TFLOP/s',
                          'frac': ach / gemm_peak()[0], 'gemm': gemm_peak()[1], 'traffic': _traffic('train88'),
@@ -200,7 +381,7 @@ def bench_blazeface(dev, iters, no_cpu):
                         'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
                         'frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
                         'traffic': _traffic('blazeface'),
-                        'kernel': 'bf_stem_kernel + 16 bf_block_kernel + 2 head GEMMs + 2 regressor '
+                        'kernel': 'bf_stem_kernel + bf_* blocks + 2 head GEMMs + 2 regressor '
                                   'programs (hpe_blazeface_forward + hpe_forward)',
                         'kernel_ms': ms, 'bytes_per_launch': nbytes * BLAZE_B,
                         'flop_per_launch': flop * BLAZE_B,
@@ -208,11 +389,9 @@ def bench_blazeface(dev, iters, no_cpu):
     if not no_cpu:
         sys.path.insert(0, ROOT)
         from oracle import keras_ref as K
-        threads = min(16, os.cpu_count() or 1)
-        torch.set_num_threads(threads)
         gr = K.Graph(mc, wts, dtype=torch.float32)
         xs = np.random.default_rng(0).uniform(-1, 1, (8, 128, 128, 3)).astype(np.float32)
-        gr.forward(xs)
+        threads, _ = _threads_for_cpu(lambda: gr.forward(xs))
         t0 = time.perf_counter()
         k = 0
         while time.perf_counter() - t0 < 10.0 or k < 2:
@@ -223,6 +402,49 @@ def bench_blazeface(dev, iters, no_cpu):
                                'sample': '%d forwards x 8 frames (oracle/keras_ref.py torch-CPU fp32), %.1f s'
                                          % (k, dt)}
     return res
+
+
+def bench_infer(hpe, dev, steps):
+    """configs[1]: hrchr82r forward, batch 256 of 96x96 maps."""
+    gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
+    with open(os.path.join(gdir, 'hrchr82r.json')) as fh:
+        mc = json.load(fh)['model_config']
+    wts = dict(np.load(os.path.join(gdir, 'hrchr82r.npz')))
+    im = hpe.model_from_config(mc, wts)
+    ie = im._eng()
+    P = H * W
+    xi, _ = synth(INFER_B, 99, dev)
+    yo = torch.empty((INFER_B * P, 3), device=dev)
+    for _ in range(3):
+        ie.forward(xi, P, out=yo)
+    torch.cuda.synchronize()
+    es = []
+    t0 = time.perf_counter()
+    n_inf = max(10, steps)
+    for _ in range(n_inf):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ie.forward(xi, P, out=yo)
+        e1.record()
+        es.append((e0, e1))
+    torch.cuda.synchronize()
+    idt = time.perf_counter() - t0
+    ims = float(np.mean([s.elapsed_time(e) for s, e in es]))
+    bytes_launch = INFER_BYTES_POS * INFER_B * P
+    return {
+        'workload': 'Model-96 hrchr82r head (96-32-16-3, reference weights) forward, batch 256, '
+                    '96x96 maps (configs[1])',
+        'value': INFER_B * n_inf / idt, 'unit': 'images/sec', 'ms_per_batch': idt * 1e3 / n_inf,
+        'roofline': {'bound': 'hbm', 'achieved': bytes_launch / (ims * 1e-3) / 1e9,
+                     'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
+                     'frac': bytes_launch / (ims * 1e-3) / PEAK_HBM,
+                     'traffic': _traffic('infer'),
+                     'kernel': {'chain': 'chain_split_kernel (+ guarded chain_fwd_kernel)',
+                                'generic': 'rowprog_kernel'}.get(ie.program('fwd', P).prog.kind, '?')
+                     + ' (hpe_forward)',
+                     'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
+                     'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
 
 
 def _cpu_name():
@@ -247,7 +469,7 @@ def _traffic(kind):
         return None
 
 
-def main():
+def parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
@@ -256,11 +478,27 @@ def main():
     ap.add_argument('--no-infer', action='store_true')
     ap.add_argument('--no-blaze', action='store_true')
     ap.add_argument('--no-train88', action='store_true')
-    a = ap.parse_args()
+    ap.add_argument('--no-strong', action='store_true')
+    ap.add_argument('--no-p1', action='store_true')
+    ap.add_argument('--only', default='', help='comma list of lines to run (train,strong,p1,infer,train88,blazeface)')
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if launch_plan(a.gpus, argv, os.environ) is not None:
+        sys.exit(spawn_ranks(a.gpus, argv))
+    only = set(x for x in a.only.split(',') if x)
+
+    def want(name, flag=False):
+        return (name in only) if only else not flag
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus and 'WORLD_SIZE' in os.environ:
+        print('bench.py: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE' % (a.gpus, world), file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     dist = None
@@ -272,129 +510,64 @@ def main():
     from hpe import keras
     hpe.set_seed(42)
     keras.backend.clear_session()
-    m = build_train_model(hpe, keras)
+    m = build_train_model(keras)
     init_w = m.weights_dict()
     eng = m._eng()
-    x, y = synth(PER_GPU, 1234 + rank, dev)
     P = H * W
     n_global = PER_GPU * world
-    inv_count = 1.0 / (n_global * P * 3)
-    stats = torch.zeros((a.steps + a.warmup + 1, 2 + eng.optim_grid()), device=dev)
-
-    def step(i):
-        eng.gradient(x, y, P, None, PER_GPU, inv_count, seed=i + 1, img_off=rank * PER_GPU)
-        if dist is not None:
-            dist.all_reduce(eng.grad)
-        eng.optimizer_step(m.optimizer, stats[i])
-
-    for i in range(a.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # per-launch timing of the dominant kernel with events on the launch stream (in-loop, cheap)
-    starts, ends = [], []
-    for i in range(a.steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        eng.gradient(x, y, P, None, PER_GPU, inv_count, seed=a.warmup + i + 1, img_off=rank * PER_GPU)
-        e1.record()
-        starts.append(e0)
-        ends.append(e1)
-        if dist is not None:
-            dist.all_reduce(eng.grad)
-        eng.optimizer_step(m.optimizer, stats[a.warmup + i])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    train_ms = float(np.mean(kernel_ms))  # train_step kernel + its reduce kernel
-    loss_mse = float(stats[a.warmup + a.steps - 1, 0].item()) / (n_global * P * 3)
-
-    out = None
-    if rank == 0:
-        ips = n_global * a.steps / dt
+    out = {'metric': METRIC, 'unit': 'images/sec', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+           'data': 'synthetic (96x96x96 post-ReLU-like features, random-init weights)',
+           'config': {'workload': 'Model-96 create_model(num_filters=360, dropout=0, l2=0.1) '
+                                  'training, legacy Adam lr 2.8e-4, 96x96 feature maps '
+                                  '(configs[3] per GPU: 512 images per rank)',
+                      'global_batch': n_global, 'per_gpu_batch': PER_GPU, 'positions_per_image': P,
+                      'channels': C, 'parallelism': 'dp%d' % world},
+           'world_size_seen': dist.get_world_size() if dist is not None else 1,
+           'backend': dist.get_backend() if dist is not None else 'none (single process)'}
+    if want('train'):
+        x, y = synth(PER_GPU, 1234 + rank, dev)
+        dt, train_ms, mse = run_train(eng, m.optimizer, x, y, P, PER_GPU, n_global, rank, world,
+                                      a.steps, a.warmup, dist)
+        del x, y
         flop_launch = TRAIN_FLOP_POS * PER_GPU * P
         achieved = flop_launch / (train_ms * 1e-3)
-        out = {
-            'metric': METRIC, 'value': ips, 'unit': 'images/sec', 'n_gpus': world,
-            'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': dt * 1e3 / a.steps,
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
-            'data': 'synthetic (96x96x96 post-ReLU-like features, random-init weights)',
-            'config': {'workload': 'Model-96 create_model(num_filters=360, dropout=0, l2=0.1) '
-                                   'training, legacy Adam lr 2.8e-4, 96x96 feature maps '
-                                   '(configs[3] per GPU)',
-                       'global_batch': n_global, 'positions_per_image': P, 'channels': C,
-                       'parallelism': 'dp%d' % world},
+        out.update({
+            'value': n_global * a.steps / dt, 'ms_per_step': dt * 1e3 / a.steps,
             'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': gemm_peak()[0] / 1e12,
                          'unit': 'TFLOP/s', 'frac': achieved / gemm_peak()[0], 'gemm': gemm_peak()[1],
                          'traffic': _traffic('train'),
                          'kernel': {'mlp2': 'mlp2_kernel', 'generic': 'rowprog_kernel'}.get(
                              eng.program('train', P).prog.kind, '?') + ' + reduce_kernel (hpe_train_step + hpe_reduce)',
                          'kernel_ms': train_ms, 'flop_per_launch': flop_launch},
-            'train_mse_last_step': loss_mse,
-        }
-    # ---- inference line (configs[1]) -----------------------------------------------------
-    if rank == 0 and not a.no_infer:
-        import json as _j
-        gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
-        with open(os.path.join(gdir, 'hrchr82r.json')) as fh:
-            mc = _j.load(fh)['model_config']
-        wts = dict(np.load(os.path.join(gdir, 'hrchr82r.npz')))
-        im = hpe.model_from_config(mc, wts)
-        ie = im._eng()
-        xi, _ = synth(INFER_B, 99, dev)
-        yo = torch.empty((INFER_B * P, 3), device=dev)
-        for _ in range(3):
-            ie.forward(xi, P, out=yo)
-        torch.cuda.synchronize()
-        es = []
-        t0 = time.perf_counter()
-        n_inf = max(10, a.steps)
-        for _ in range(n_inf):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ie.forward(xi, P, out=yo)
-            e1.record()
-            es.append((e0, e1))
-        torch.cuda.synchronize()
-        idt = time.perf_counter() - t0
-        ims = float(np.mean([s.elapsed_time(e) for s, e in es]))
-        bytes_launch = INFER_BYTES_POS * INFER_B * P
-        out['infer'] = {
-            'workload': 'Model-96 hrchr82r head (96-32-16-3, reference weights) forward, batch 256, '
-                        '96x96 maps (configs[1])',
-            'value': INFER_B * n_inf / idt, 'unit': 'images/sec', 'ms_per_batch': idt * 1e3 / n_inf,
-            'roofline': {'bound': 'hbm', 'achieved': bytes_launch / (ims * 1e-3) / 1e9,
-                         'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
-                         'frac': bytes_launch / (ims * 1e-3) / PEAK_HBM,
-                         'traffic': _traffic('infer'),
-                         'kernel': {'chain': 'chain_split_kernel (+ guarded chain_fwd_kernel)', 'generic': 'rowprog_kernel'}.get(
-                             ie.program('fwd', P).prog.kind, '?') + ' (hpe_forward)',
-                         'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
-                         'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
-    # ---- Model-88 on 88x88 maps (north_star's second map size) --------------------------------
-    if rank == 0 and not a.no_train88:
+            'train_mse_last_step': mse})
+    if want('strong', a.no_strong):
+        # configs[3] as written: global batch 4096 split over the ranks (strong scaling)
+        n_loc = STRONG_GLOBAL // world
+        m.set_weights(init_w)
+        x, y = synth(n_loc, 4321 + rank, dev)
+        st = max(3, a.steps // 4)
+        dt, kms, _ = run_train(eng, m.optimizer, x, y, P, n_loc, n_loc * world, rank, world, st,
+                               min(2, a.warmup), dist)
+        del x, y
+        out['strong'] = {'workload': 'configs[3]: global batch %d images of 96x96 split over %d rank(s) '
+                                     '(%d per rank), same model / optimizer' % (n_loc * world, world, n_loc),
+                         'value': n_loc * world * st / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3 / st,
+                         'steps': st, 'scaling': 'strong', 'kernel_ms': kms}
+    if rank == 0 and want('p1', a.no_p1) and world == 1:
+        out['p1'] = bench_p1(keras, no_cpu=a.no_cpu)
+    if rank == 0 and want('infer', a.no_infer):
+        out['infer'] = bench_infer(hpe, dev, a.steps)
+    if rank == 0 and want('train88', a.no_train88):
         out['train88'] = bench_train88(hpe, keras, dev, max(5, min(a.steps, 20)), 2)
-    # ---- BlazeFace + both pose heads ----------------------------------
-    if rank == 0 and not a.no_blaze:
+    if rank == 0 and want('blazeface', a.no_blaze):
         out['blazeface'] = bench_blazeface(dev, max(10, a.steps), a.no_cpu or world > 1)
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if rank == 0 and world == 1 and want('train') and not a.no_cpu:
         cb = cpu_baseline((m.model_config, init_w))
         out['cpu_baseline'] = cb
         out['vs_cpu_baseline'] = out['value'] / cb['value']
     if rank == 0:
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -179,7 +179,8 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
 }
 
 
-// The same chain on fp16 MFMA at fp32 accuracy (split8 / mfma3, hpe_common.h): layer 1 as six
+// The same chain on fp16 MFMA at fp32 accuracy (split_w8 / split_d8 / mfma3_wd, hpe_common.h:
+// exponent-shifted lo halves, accumulators at scale SPLIT_C, unscaled in the bias fma): layer 1 as six
 // K-steps of three v_mfma_f32_32x32x16_f16 (576 MFMA cycles per 32-row tile instead of 3,072 on
 // v_mfma_f32_32x32x2_f32), layer 2 as two, the head on the VALU in fp32 as above.  With the MFMA
 // work cut 5x the kernel is bound by the X stream alone.  A tile whose accumulators come out
@@ -216,28 +217,47 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
   if (threadIdx.x < 4) tb3[threadIdx.x] = (threadIdx.x < 3 && o[O_TBASE] >= 0) ? P_[o[O_TBASE] + threadIdx.x] : 0.f;
 
   // A of layer 1: W1^T[n = l32][k], K-step s holds k = 16 s + 8 half + j (j = 0..7)
-  h8 w1h[6], w1l[6];
+  // weight-side exponents (pow2_scale, hpe_common.h): W1 and W2 each enter their MFMAs scaled by
+  // one power of two (their max |w| in [2^13, 2^14)); layer outputs come out as acc * inv
+  SplitW w1[6];
+  float inv1, inv2;
+  {
+    f32x8 v[6];
+    float mx = 0.f;
 #pragma unroll
-  for (int s = 0; s < 6; ++s) {
-    f32x8 v;
+    for (int s = 0; s < 6; ++s) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 16 * s + 8 * half + j;
-      const float t = P_[o[O_W] + (size_t)min(k, Cin - 1) * F1 + min(l32, F1 - 1)];
-      v[j] = (k < Cin && l32 < F1) ? t : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + 8 * half + j;
+        const float t = P_[o[O_W] + (size_t)min(k, Cin - 1) * F1 + min(l32, F1 - 1)];
+        v[s][j] = (k < Cin && l32 < F1) ? t : 0.f;
+        mx = fmaxf(mx, fabsf(v[s][j]));
+      }
     }
-    split8(v, w1h[s], w1l[s]);
+    const float sc = pow2_scale(wave_max(mx), 13);
+    inv1 = SPLIT_INV_C / sc;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) w1[s] = split_w8(v[s] * sc);
   }
   __syncthreads();
   // A of layer 2: W2^T[m = l32][n], in the k order of an accumulator used as the B operand:
   // element j of K-step s of lane half h <-> hidden unit 16 s + 8 (j >> 2) + 4 h + (j & 3)
-  h8 w2h[2], w2l[2];
+  SplitW w2[2];
+  {
+    f32x8 v[2];
+    float mx = 0.f;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    f32x8 v;
+    for (int s = 0; s < 2; ++s) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tw2[(16 * s + 8 * (j >> 2) + 4 * half + (j & 3)) * 32 + l32];
-    split8(v, w2h[s], w2l[s]);
+      for (int j = 0; j < 8; ++j) {
+        v[s][j] = tw2[(16 * s + 8 * (j >> 2) + 4 * half + (j & 3)) * 32 + l32];
+        mx = fmaxf(mx, fabsf(v[s][j]));
+      }
+    }
+    const float sc = pow2_scale(wave_max(mx), 13);
+    inv2 = SPLIT_INV_C / sc;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) w2[s] = split_w8(v[s] * sc);
   }
   float b1r[16];
 #pragma unroll
@@ -282,13 +302,11 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
       const int c0 = 4 * s + 2 * half;
       const f32x4 a0 = *(const f32x4*)(xr + 4 * (c0 ^ sw));
       const f32x4 a1 = *(const f32x4*)(xr + 4 * ((c0 + 1) ^ sw));
-      h8 xh, xl;
-      split8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, xh, xl);
-      acc = mfma3(w1h[s], w1l[s], xh, xl, acc);
+      acc = mfma3_wd(w1[s], split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), acc);
     }
     float chk = sum16(acc);
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, acc[g] + b1r[g]);
+    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, fmaf(acc[g], inv1, b1r[g]));
     int toff = 0;
     asm volatile("" : "+v"(toff));
     // ---- layer 2 (optional): B = A1^T straight from the accumulator registers 8 s .. 8 s + 7 ----
@@ -297,16 +315,15 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
       f32x16 acc2 = {};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        h8 ah, al;
-        split8(f32x8{acc[8 * s + 0], acc[8 * s + 1], acc[8 * s + 2], acc[8 * s + 3],
-                     acc[8 * s + 4], acc[8 * s + 5], acc[8 * s + 6], acc[8 * s + 7]}, ah, al);
-        acc2 = mfma3(w2h[s], w2l[s], ah, al, acc2);
+        acc2 = mfma3_wd(w2[s], split_d8(f32x8{acc[8 * s + 0], acc[8 * s + 1], acc[8 * s + 2], acc[8 * s + 3],
+                                              acc[8 * s + 4], acc[8 * s + 5], acc[8 * s + 6], acc[8 * s + 7]}),
+                        acc2);
       }
       chk += sum16(acc2);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
-        acc2[g] = cact<A2>(act2, acc2[g] + tb2[toff + mm]);
+        acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
       }
       h = acc2;
     }

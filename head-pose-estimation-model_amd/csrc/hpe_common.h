@@ -119,6 +119,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
 struct Args {
   const int* prog;
   const float* params;
@@ -138,26 +144,71 @@ struct Args {
 };
 
 // ------------------------------------------------------------------------------------------------
-// fp32 GEMMs on fp16 MFMA at fp32 accuracy ("3 x fp16 split"): a = a_hi + a_lo, b = b_hi + b_lo
-// with fp16 halves (a_lo = fp16(a - a_hi) is exact to 2^-22 |a|), a.b ~= a_hi.b_hi + a_hi.b_lo +
-// a_lo.b_hi (the dropped a_lo.b_lo is ~2^-22 relative), fp32 accumulate.  Three
-// v_mfma_f32_32x32x16_f16 (32 cycles each) per 16 of K replace eight v_mfma_f32_32x32x2_f32
-// (64 cycles each): 5.3x the MFMA rate of the exact-fp32 instruction.  Range: |a|, |b| < 65504
-// (an fp16 overflow makes the accumulator non-finite; kernels using this check it and hand the
-// launch to their exact-fp32 twin, see Args::guard).
+// fp32 GEMMs on fp16 MFMA at fp32 accuracy ("3 x fp16 split", exponent-shifted):
+//   w = w_h + w_l, d = d_h + d_l with fp16 halves; w.d ~= w_h.d_h + w_h.d_l + w_l.d_h (the dropped
+//   w_l.d_l is <= 2^-22 relative).  A plain fp16 lo half (|lo| ~ 2^-11 |v|) is subnormal below
+//   |v| ~ 2^-3 and loses bits there, so both lo halves are carried scaled by C = 2^SPLIT_SHIFT
+//   and the whole product is accumulated at scale C:
+//     weight side (2 fragments)  h  = fp16(w),       cl = fp16(C (w - h))
+//     data side   (3 fragments)  ch = fp16(C d),     cl = fp16(C d - ch),    h = fp16(d)
+//     C w.d ~= ch.h_w + h.cl_w + cl.h_w          (three v_mfma_f32_32x32x16_f16)
+//   and the consumer multiplies the accumulator by 1/C (folded into its bias fma / flush scale).
+//   Every fragment is a normal fp16 number for |w|, |d| >= 2^-2 / C (2.4e-4), so the relative
+//   error per product stays at the fp32 level down there; below it the absolute error is
+//   <= 2^-25 / C.  Range: |d| < 65504 / C (64; the reference's features stay below 10.4), |w| <
+//   65504: an fp16 overflow makes the accumulator non-finite; kernels using this check it and
+//   hand the launch to their exact-fp32 twin (Args::guard).  Three v_mfma_f32_32x32x16_f16 (32
+//   cycles each) per 16 of K replace eight v_mfma_f32_32x32x2_f32 (64 cycles each).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ void split8(f32x8 v, h8& hi, h8& lo) {
-  hi = __builtin_convertvector(v, h8);
-  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), h8);
+#define SPLIT_SHIFT 10
+#define SPLIT_C 1024.0f
+#define SPLIT_INV_C (1.0f / 1024.0f)
+
+struct SplitW { h8 h, cl; };       // weight side: fp16(w), fp16(C (w - h))
+struct SplitD { h8 ch, cl, h; };   // data side:   fp16(C d), fp16(C d - ch), fp16(d)
+
+__device__ __forceinline__ SplitW split_w8(f32x8 v) {
+  SplitW r;
+  r.h = __builtin_convertvector(v, h8);
+  r.cl = __builtin_convertvector((v - __builtin_convertvector(r.h, f32x8)) * SPLIT_C, h8);
+  return r;
 }
 
-__device__ __forceinline__ f32x16 mfma3(h8 ah, h8 al, h8 bh, h8 bl, f32x16 acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+__device__ __forceinline__ SplitD split_d8(f32x8 v) {
+  SplitD r;
+  const f32x8 s = v * SPLIT_C;
+  r.ch = __builtin_convertvector(s, h8);
+  r.cl = __builtin_convertvector(s - __builtin_convertvector(r.ch, f32x8), h8);
+  r.h = __builtin_convertvector(v, h8);
+  return r;
+}
+
+// Power-of-two scale s with m s in [2^t, 2^(t+1)) (1 for m == 0 or a non-finite m): applied to a
+// weight-side operand before split_w8 (per MFMA column, e.g. one W1 column) so its largest value
+// sits near 2^t and its small values keep normal fp16 hi halves (a plain fp16 hi is subnormal
+// below 6.1e-5, where 28 % of an L2 = 0.1 checkpoint's W1 lies); the consumer unscales by 1/s.
+__device__ __forceinline__ float pow2_scale(float m, int t) {
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 1.f;
+  int e;
+  frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+  e = e > 100 ? 100 : (e < -100 ? -100 : e);
+  return ldexpf(1.f, t + 1 - e);
+}
+
+// acc += C (D.W) with the data fragments as the MFMA A operand (rows) and the weights as B
+__device__ __forceinline__ f32x16 mfma3_dw(const SplitD& d, const SplitW& w, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(d.cl, w.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(d.h, w.cl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(d.ch, w.h, acc, 0, 0, 0);
+}
+// acc += C (W.D) with the weights as the A operand and the data fragments as B
+__device__ __forceinline__ f32x16 mfma3_wd(const SplitW& w, const SplitD& d, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h, d.cl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.cl, d.h, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h, d.ch, acc, 0, 0, 0);
 }
 
 __device__ __forceinline__ float sum16(const f32x16& a) {

@@ -25,17 +25,20 @@
 #define MLP2_XS 100             // LDS row stride of an X tile (floats): conflict-free, 16-B aligned
 #define MLP2_XF (32 * MLP2_XS)  // floats per X tile buffer
 #define MLP2_LAB 128            // floats per label buffer: [32 rows][4] (yaw, pitch, roll, pad)
-// pre-split X tiles (SPLIT kernels of the 12-wave variant, see presplit_tile): fp16 hi / lo halves
+// pre-split X tiles (SPLIT kernels of the 12-wave variant, see presplit_tile): the three fp16
+// fragments of the data side of split_d8 (hpe_common.h): ch = fp16(C x), cl = fp16(C x - ch), h = fp16(x)
 #define MLP2_FS 104             // row stride (halves) of the forward layout [32 rows][2 x 48]: conflict-free b128
 #define MLP2_TS 40              // row stride (halves) of the transposed layout [96 channels][32 rows]
-#define MLP2_PRE_HALVES (2 * 32 * MLP2_FS + 4 * 96 * MLP2_TS)  // fwd hi, lo + 2 parities x transposed hi, lo
+#define MLP2_PRE_HALVES (3 * 32 * MLP2_FS + 2 * 3 * 96 * MLP2_TS)  // fwd ch, cl, h + 2 parities x transposed ch, cl, h
 
 // LDS-DMA (global_load_lds) in inline asm: hipcc's waitcnt pass cannot tell the two X buffers
 // apart and would put vmcnt(0) before every ds_read of the tile in use, draining the prefetch of
 // the next one; hidden from it, the prefetch completes only at the explicit vmcnt(0) before the
 // barrier that opens its tile.  M0 is written in the same statement (compiler-reserved).
+// the low 32 bits of a flat (generic) pointer into LDS are the LDS byte address (the high half is
+// the shared aperture); no generic -> local addrspacecast (its null check miscompiles on constants)
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
-  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p);
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
 __device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_dst) {
   unsigned keep;
@@ -169,38 +172,50 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 // One split of the landed X tile per workgroup instead of one per wave (the 12 waves all read the
-// whole tile, in two layouts): every thread turns 4 floats into fp16 hi / lo halves, written
+// whole tile, in two layouts): every thread turns 4 floats into the three data-side fp16 fragments
+// (ch, cl, h of split_d8), written
 //   * forward layout  xf[r][48 h + m] = X[r][KH h + m] (zero for m >= KH): lane (row r, half h)
-//     reads K-step s as one b128 at 48 h + 8 s;
+//     reads K-step s as one b128 per fragment at 48 h + 8 s; fragment f at xf + f * 32 * FS;
 //   * transposed      xt[k][p(r)] = X[r][k], p(r) = r with bits 2 and 3 swapped, so the 8 rows
 //     16 s + 8 (j >> 2) + 4 h + (j & 3) of the dW1 K-step s are the contiguous p = 16 s + 8 h + j:
-//     one b128 per (K-step, 32-channel block) instead of 8 strided b32 reads + a split per wave.
+//     one b128 per (K-step, 32-channel block, fragment) instead of 8 strided b32 reads + a split per
+//     wave; fragment f at xt + f * 96 * TS.
 // Pad channels [C_in, 96) of the raw tile hold zeros, so their xt rows are zero.
+__device__ __forceinline__ void split_d4(f32x4 v, h4& ch, h4& cl, h4& h) {
+  const f32x4 s = v * SPLIT_C;
+  ch = __builtin_convertvector(s, h4);
+  cl = __builtin_convertvector(s - __builtin_convertvector(ch, f32x4), h4);
+  h = __builtin_convertvector(v, h4);
+}
 template <int KH>
-__device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xfh, _Float16* xfl, _Float16* xth,
-                                              _Float16* xtl, int tid, int NT) {
+__device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xf, _Float16* xt, int tid, int NT) {
   for (int i = tid; i < 32 * 24; i += NT) {
     const int r = i / 24, rem = i - r * 24, h = rem >= 12 ? 1 : 0, m0 = 4 * (rem - 12 * h);
     const f32x4 v = m0 < KH ? *(const f32x4*)(xs + r * MLP2_XS + KH * h + m0) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const h4 hi = __builtin_convertvector(v, h4);
-    const h4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), h4);
-    *(h4*)(xfh + r * MLP2_FS + 48 * h + m0) = hi;
-    *(h4*)(xfl + r * MLP2_FS + 48 * h + m0) = lo;
+    h4 ch, cl, hh;
+    split_d4(v, ch, cl, hh);
+    _Float16* d = xf + r * MLP2_FS + 48 * h + m0;
+    *(h4*)(d) = ch;
+    *(h4*)(d + 32 * MLP2_FS) = cl;
+    *(h4*)(d + 64 * MLP2_FS) = hh;
   }
   for (int i = tid; i < 96 * 8; i += NT) {
     const int rg = i / 96, k = i - rg * 96, r = 4 * rg;
     const f32x4 v = {xs[r * MLP2_XS + k], xs[(r + 1) * MLP2_XS + k], xs[(r + 2) * MLP2_XS + k],
                      xs[(r + 3) * MLP2_XS + k]};
     const int p = (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);
-    const h4 hi = __builtin_convertvector(v, h4);
-    const h4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), h4);
-    *(h4*)(xth + k * MLP2_TS + p) = hi;
-    *(h4*)(xtl + k * MLP2_TS + p) = lo;
+    h4 ch, cl, hh;
+    split_d4(v, ch, cl, hh);
+    _Float16* d = xt + k * MLP2_TS + p;
+    *(h4*)(d) = ch;
+    *(h4*)(d + 96 * MLP2_TS) = cl;
+    *(h4*)(d + 192 * MLP2_TS) = hh;
   }
 }
 
 // NWM: launch bound in waves (12: any width <= 384, 168-VGPR budget; 4: F <= 128, 256 budget)
-// SPLIT: both GEMMs on fp16 MFMA at fp32 accuracy (split8 / mfma3, hpe_common.h), same registers:
+// SPLIT: both GEMMs on fp16 MFMA at fp32 accuracy (split_w8 / split_d8 / mfma3_dw, hpe_common.h:
+//   exponent-shifted lo halves, X the 3-fragment data side, accumulators at scale SPLIT_C), same registers:
 //   forward  Z1 = X.W1: 6 K-steps of three v_mfma_f32_32x32x16_f16 (576 MFMA cycles per wave per
 //            tile instead of 48 x 64 = 3,072); K-step s, lane half h, element j <-> channel
 //            KH h + 8 s + j, so a lane splits 8 contiguous X floats of its row (two ds_read_b128) and
@@ -243,9 +258,8 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
   float* red = hacc + NCB * 256;  // [NCB * 64]
-  _Float16* xfh = (_Float16*)(red + NCB * 64);  // PRE: [32][MLP2_FS] hi, lo; [2][96][MLP2_TS] hi, lo
-  _Float16* xfl = xfh + 32 * MLP2_FS;
-  _Float16* xtb = xfl + 32 * MLP2_FS;
+  _Float16* xfb = (_Float16*)(red + NCB * 64);  // PRE: [3][32][MLP2_FS] ch, cl, h; [2][3][96][MLP2_TS]
+  _Float16* xtb = xfb + 3 * 32 * MLP2_FS;
 
   E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
   E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
@@ -255,19 +269,32 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 
   // ---- register-resident weights of this wave's 32 hidden columns ----
   float wreg[SPLIT ? 1 : KH];
-  h8 wh[SPLIT ? 6 : 1], wl[SPLIT ? 6 : 1];
+  SplitW wsp[SPLIT ? 6 : 1];
+  // SPLIT: weight-side exponents per hidden unit n (pow2_scale): W1 column n enters the forward
+  // MFMAs scaled by s1 (its max |w| in [2^13, 2^14)), Z1 comes out as acc * inv1, inv1 = 1 / (C s1);
+  // dZ1 column n enters the dW1 MFMAs scaled by s2 (from max_j |W2[n][j]|, its only per-column
+  // factor: s2 max |W2[n]| in [2^2, 2^3)), dW1 leaves as acc / (C s2)
+  float inv1 = 1.f, s2 = 1.f;
   if constexpr (SPLIT) {
+    f32x8 v[6];
+    float mx = 0.f;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
-      f32x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = half * KH + 8 * s + j;
         const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
-        v[j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
+        v[s][j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
+        mx = fmaxf(mx, fabsf(v[s][j]));
       }
-      split8(v, wh[s], wl[s]);
     }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float s1 = pow2_scale(mx, 13);
+    inv1 = SPLIT_INV_C / s1;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wsp[s] = split_w8(v[s] * s1);
+    const float* w2n = args.params + o[O_AUX0] + min(n, F - 1) * 3;
+    s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
   } else {
 #pragma unroll
     for (int m = 0; m < KH; ++m) {
@@ -317,7 +344,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   if constexpr (PRE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar_lds();
-    presplit_tile<KH>(xbuf, xfh, xfl, xtb, xtb + 96 * MLP2_TS, threadIdx.x, NT);
+    presplit_tile<KH>(xbuf, xfb, xtb, threadIdx.x, NT);
   }
   int buf = 0;
 #ifdef MLP2_STAMPS
@@ -352,11 +379,12 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       const float* ap = xs + l32 * MLP2_XS + half * KH;
       f32x16 acc = {};
       if constexpr (PRE) {
-        const _Float16* fh = xfh + l32 * MLP2_FS + 48 * half;
-        const _Float16* fl = xfl + l32 * MLP2_FS + 48 * half;
+        const _Float16* fp = xfb + l32 * MLP2_FS + 48 * half;
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
-          acc = mfma3(*(const h8*)(fh + 8 * s), *(const h8*)(fl + 8 * s), wh[s], wl[s], acc);
+          const SplitD xd = {*(const h8*)(fp + 8 * s), *(const h8*)(fp + 32 * MLP2_FS + 8 * s),
+                             *(const h8*)(fp + 64 * MLP2_FS + 8 * s)};
+          acc = mfma3_dw(xd, wsp[s], acc);
           __builtin_amdgcn_sched_barrier(0);
         }
         bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
@@ -365,9 +393,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
           const f32x4 a0 = *(const f32x4*)(ap + 8 * s), a1 = *(const f32x4*)(ap + 8 * s + 4);
-          h8 xh, xl;
-          split8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, xh, xl);
-          acc = mfma3(xh, xl, wh[s], wl[s], acc);
+          acc = mfma3_dw(split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), wsp[s], acc);
           __builtin_amdgcn_sched_barrier(0);
         }
         bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
@@ -404,7 +430,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        float z = act1_f<ACT1>(e1.act, acc[g] + b1);
+        float z = act1_f<ACT1>(e1.act, SPLIT ? fmaf(acc[g], inv1, b1) : acc[g] + b1);
         if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
         acc[g] = nok ? z : 0.f;
       }
@@ -485,8 +511,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       bar_lds();
       STAMP(7);
       if (tile + gridDim.x < ntiles) {
-        _Float16* xt = xtb + (buf ^ 1) * 2 * 96 * MLP2_TS;
-        presplit_tile<KH>(xbuf, xfh, xfl, xt, xt + 96 * MLP2_TS, threadIdx.x, NT);
+        presplit_tile<KH>(xbuf, xfb, xtb + (buf ^ 1) * 3 * 96 * MLP2_TS, threadIdx.x, NT);
       }
       if (!train) continue;
     } else {
@@ -521,26 +546,26 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
       if constexpr (PRE) {
         // dZ1 of K-step 0 -> split -> its 9 MFMAs, with the VALU of K-step 1's dZ1 free to issue
         // under them (no scheduling fences between the two), then K-step 1's MFMAs
-        const _Float16* th = xtb + buf * 2 * 96 * MLP2_TS + l32 * MLP2_TS + 8 * half;
+        const _Float16* th = xtb + buf * 3 * 96 * MLP2_TS + l32 * MLP2_TS + 8 * half;
         f32x8 dv0, dv1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) dv0[j] = dz_of(j);
-        h8 d0h, d0l;
-        split8(dv0, d0h, d0l);
+        const SplitW d0 = split_w8(dv0 * s2);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-          dw[kb] = mfma3(*(const h8*)(th + kb * 32 * MLP2_TS), *(const h8*)(th + (96 + kb * 32) * MLP2_TS),
-                         d0h, d0l, dw[kb]);
+        for (int kb = 0; kb < NKB; ++kb) {
+          const _Float16* q = th + kb * 32 * MLP2_TS;
+          dw[kb] = mfma3_dw(SplitD{*(const h8*)(q), *(const h8*)(q + 96 * MLP2_TS), *(const h8*)(q + 192 * MLP2_TS)}, d0, dw[kb]);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) dv1[j] = dz_of(8 + j);
         __builtin_amdgcn_sched_barrier(0);
-        h8 d1h, d1l;
-        split8(dv1, d1h, d1l);
+        const SplitW d1 = split_w8(dv1 * s2);
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-          dw[kb] = mfma3(*(const h8*)(th + 16 + kb * 32 * MLP2_TS), *(const h8*)(th + 16 + (96 + kb * 32) * MLP2_TS),
-                         d1h, d1l, dw[kb]);
+        for (int kb = 0; kb < NKB; ++kb) {
+          const _Float16* q = th + 16 + kb * 32 * MLP2_TS;
+          dw[kb] = mfma3_dw(SplitD{*(const h8*)(q), *(const h8*)(q + 96 * MLP2_TS), *(const h8*)(q + 192 * MLP2_TS)}, d1, dw[kb]);
+        }
       } else if constexpr (SPLIT) {
         // K-step s (rows 16 s + 8 (j >> 2) + 4 h + (j & 3)): dZ1 registers 8 s .. 8 s + 7 as the B
         // operand, the matching X^T rows as A; one K-step at a time keeps the live set small
@@ -552,17 +577,14 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
             dv[j] = dz_of(8 * s + j);
             if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
           }
-          h8 dh, dl;
-          split8(dv, dh, dl);
+          const SplitW dsp = split_w8(dv * s2);
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) {
             const float* xp = xs + (4 * half) * MLP2_XS + kb * 32 + l32;
             f32x8 xv;
 #pragma unroll
             for (int j = 0; j < 8; ++j) xv[j] = xp[(16 * s + 8 * (j >> 2) + (j & 3)) * MLP2_XS];
-            h8 th, tl;
-            split8(xv, th, tl);
-            dw[kb] = mfma3(th, tl, dh, dl, dw[kb]);
+            dw[kb] = mfma3_dw(split_d8(xv), dsp, dw[kb]);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -617,7 +639,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * sc;
+        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (SPLIT ? sc * (SPLIT_INV_C / s2) : sc);
       }
     }
     if (SPLIT) bad |= !(fabsf(chk) <= 3.0e38f);
