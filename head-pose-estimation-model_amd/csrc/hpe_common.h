@@ -231,5 +231,10 @@ int chain_grid_cap(int n_cu);
 int chain_lds_bytes();
 int chain_launch(const int* words_host, const Args& a, int grid, hipStream_t s);
 
+// a program's word stream: host copy (kernel geometry) and device copy (kernel argument)
+struct hpe_program;
+const int* hpe_prog_words(const hpe_program* p);
+const int* hpe_prog_dwords(const hpe_program* p);
+
 // thread-local error message of the C ABI (hpe_last_error); returns code
 int hpe_fail(int code, const char* fmt, ...);

@@ -1,0 +1,55 @@
+// hpe_dev.h — device helpers shared by the fused regressor kernels (hpe_mlp2.hip, hpe_fit.hip):
+// LDS-DMA staging, an LDS-only workgroup barrier, and the layer-1 activations of the hot loops.
+#pragma once
+#include "hpe_common.h"
+
+// LDS-DMA (global_load_lds) in inline asm: hipcc's waitcnt pass cannot tell the two X buffers
+// apart and would put vmcnt(0) before every ds_read of the tile in use, draining the prefetch of
+// the next one; hidden from it, the prefetch completes only at the explicit vmcnt(0) before the
+// barrier that opens its tile.  M0 is written in the same statement (compiler-reserved).
+// the low 32 bits of a flat (generic) pointer into LDS are the LDS byte address (the high half is
+// the shared aperture); no generic -> local addrspacecast (its null check miscompiles on constants)
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+// raw workgroup barrier that waits for LDS traffic only: an in-flight global_load_lds prefetch of
+// the next tile survives it (__syncthreads() would drain it with vmcnt(0))
+__device__ __forceinline__ void bar_lds() {
+  asm volatile("" ::: "memory");       // no LDS access moves across it
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// activation of layer 1 fixed at compile time (tanh: Model-96, softsign: Model-88); ACT1 = -1 is
+// the runtime-dispatched variant for the other activations the checkpoints use
+// short-sequence tanh / softsign for the register-resident hot loop: tanh|z| = (1-t)/(1+t),
+// t = exp(-2|z|) via v_exp_f32; absolute error <= ~2 ulp(1.0) (covered by the atol of the parity
+// tests), derivative 1 - a^2 as in Keras' TanhGrad
+__device__ __forceinline__ float fast_tanh(float z) {
+  const float t = __expf(-2.f * fabsf(z));
+  return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), z);
+}
+template <int ACT1>
+__device__ __forceinline__ float act1_f(int act, float z) {
+  if (ACT1 == ACT_TANH) return fast_tanh(z);
+  if (ACT1 == ACT_SOFTSIGN) return z * __builtin_amdgcn_rcpf(1.f + fabsf(z));
+  return act_f(ACT1 >= 0 ? ACT1 : act, z);
+}
+template <int ACT1>
+__device__ __forceinline__ float act1_g(int act, float a) {
+  const int k = ACT1 >= 0 ? ACT1 : act;
+  return k == ACT_LINEAR ? 1.f : act_grad(k, a, 0.f);
+}
+

@@ -777,6 +777,9 @@ struct hpe_program {
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
 
+const int* hpe_prog_words(const hpe_program* p) { return p->words; }
+const int* hpe_prog_dwords(const hpe_program* p) { return p->dwords; }
+
 static int g_exact = -1;  // -1: not yet read from HPE_EXACT_FP32
 bool hpe_exact_fp32() {
   if (g_exact < 0) {

@@ -5,6 +5,7 @@ PyTorch is used only for device memory, the current HIP stream and torch.distrib
 arithmetic op of the hot path runs in libhpe.so (csrc/hpe_rowprog.hip) through the C ABI.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -76,6 +77,7 @@ class Engine:
         self.tpos = torch.from_numpy(base.tpos).to(self.device)
         self.m = None
         self.v = None
+        self._fit_ws = None
         self.iterations = 0
         self.grad = torch.zeros(self.n_train + 4, dtype=torch.float32, device=self.device)
 
@@ -187,3 +189,68 @@ class Engine:
 
     def optim_grid(self):
         return _lib.load().hpe_optim_grid(self.n_train)
+
+    # -- whole-epoch launch (P = 1, one rank): csrc/hpe_fit.hip ----------------------------------
+    def fit_epoch_supported(self, batch, P=1, world=1):
+        """True when fit's epoch can run as ONE hpe_fit_epoch launch: the reference's regime (1x1
+        maps, the 2-layer create_model family, one rank); HPE_FIT_FUSED=0 forces the per-step path."""
+        if world != 1 or P != 1 or os.environ.get('HPE_FIT_FUSED', '1') == '0':
+            return False
+        c = self.program('train', 1)
+        return c.prog.kind == 'mlp2' and _lib.load().hpe_fit_supported(c.h, int(batch)) == 1
+
+    def fit_groups(self):
+        """Workgroups of the whole-epoch launch: one per 32 hidden units."""
+        return -(-int(self.program('train', 1).prog.info['F']) // 32)
+
+    def _alphas(self, opt, steps):
+        """Per-iteration optimizer step sizes, computed exactly as hpe_optim_step does (double
+        arithmetic on the float32 hyper-parameters, rounded to float32)."""
+        t = (self.iterations + 1 + np.arange(steps)).astype(np.float64)
+        lr = float(np.float32(opt.learning_rate))
+        b1 = float(np.float32(opt.beta_1))
+        b2 = float(np.float32(opt.beta_2))
+        if opt.kind == 'adam':
+            a = lr * np.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
+        elif opt.kind == 'adamax':
+            a = lr / (1.0 - b1 ** t)
+        else:
+            a = np.full(steps, lr)
+        return torch.from_numpy(a.astype(np.float32)).to(self.device)
+
+    def fit_epoch(self, opt, x, y, perm, batch, stats, seed_base):
+        """One epoch of fit: ceil(n / batch) steps over rows perm (device int32) of x / y in one
+        launch; stats: device [steps, >= 2 + G].  A flagged fp16-split overflow re-runs the epoch
+        on the exact-fp32 path from the saved state."""
+        c = self.program('train', 1)
+        lib = _lib.load()
+        kind = OPT_KIND[opt.kind]
+        if kind and self.m is None:
+            self.m = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+            self.v = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+        n = int(perm.numel())
+        steps = -(-n // int(batch))
+        alpha = self._alphas(opt, steps)
+        need = lib.hpe_fit_workspace_size(c.h, int(batch))
+        if getattr(self, '_fit_ws', None) is None or self._fit_ws.numel() * 4 < need:
+            self._fit_ws = torch.zeros(max(need // 4, 16), dtype=torch.float32, device=self.device)
+        saved = [t.clone() for t in (self.params, self.params_t, self.m, self.v) if t is not None]
+
+        def launch(exact):
+            _lib.check(lib.hpe_fit_epoch(
+                c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v), _ptr(self.l2),
+                _ptr(self.tpos), _ptr(x), _ptr(y), _ptr(perm), n, int(batch), kind, float(opt.learning_rate),
+                float(opt.beta_1), float(opt.beta_2), float(opt.epsilon), _ptr(alpha),
+                int(seed_base) & 0xFFFFFFFFFFFFFFFF, int(self.iterations), _ptr(stats), int(stats.shape[1]),
+                int(exact), _ptr(self._fit_ws), _stream()), 'hpe_fit_epoch')
+            return int(self._fit_ws[:2].view(torch.int32)[1].item())
+
+        flags = launch(0)
+        if flags & 1:  # fp16 range exceeded somewhere: redo the epoch exactly
+            for dst, src in zip([t for t in (self.params, self.params_t, self.m, self.v) if t is not None], saved):
+                dst.copy_(src)
+            flags = launch(1)
+        if flags & 2:
+            raise _lib.HPEError('hpe_fit_epoch: workgroup exchange timed out')
+        self.iterations += steps
+        return steps

@@ -257,16 +257,24 @@ class Model:
         steps = math.ceil(n / bs)
         og = eng.optim_grid()
         stats = torch.zeros((steps, 2 + og), dtype=torch.float32, device=eng.device)
+        # the reference's regime (P = 1, create_model family, one rank): the whole epoch is one
+        # launch (csrc/hpe_fit.hip); otherwise one train_step + reduce + optimizer per step
+        fused = eng.fit_epoch_supported(bs, P, world)
+        self._last_fit_fused = fused
+        if fused:  # [sse, sae, per-wave regularisation shares of the 4 G waves]
+            stats = torch.zeros((steps, 2 + 4 * eng.fit_groups()), dtype=torch.float32, device=eng.device)
         for epoch in range(initial_epoch, epochs):
             for cb in cbs:
                 cb.on_epoch_begin(epoch)
             perm = rng.permutation(n) if shuffle else np.arange(n)
             idx = torch.from_numpy(perm.astype(np.int32)).to(eng.device)
-            nbs = []
-            for s in range(steps):
+            nbs = [min(n, (s + 1) * bs) - s * bs for s in range(steps)]
+            if fused:
+                stats.zero_()
+                eng.fit_epoch(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0))
+            for s in range(0 if fused else steps):
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0
-                nbs.append(nb)
                 r0, r1 = batch_slice(b0, b1, rank, world)   # this rank's share of the batch
                 seed = hrandom.dropout_seed(eng.iterations + 1)
                 if r1 > r0:

@@ -95,6 +95,30 @@ int hpe_optim_step(int32_t kind, float lr, float beta_1, float beta_2, float eps
 int hpe_optim_grid(int64_t n);
 
 /* ---------------------------------------------------------------------------------------------
+ * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
+ * Keras fit (train_96.py:175-183, train_88.py:355-363) for the reference's own regime: 1x1 maps
+ * (P = 1), the 2-layer create_model family (programs of kind mlp2 compiled for training), one rank.
+ * Equivalent to, for s = 0 .. ceil(n / batch) - 1 with rows perm[s*batch .. min(n, (s+1)*batch)):
+ *   hpe_train_step (dropout_seed = seed_base + iter0 + 1 + s, inv_count = 1 / (rows * 3)),
+ *   hpe_reduce, hpe_optim_step(kind, lr, beta_1, beta_2, epsilon, iter0 + 1 + s, 1.0)
+ * with alpha[s] the optimizer step size hpe_optim_step derives for that iteration (lr for SGD,
+ * lr sqrt(1-b2^t)/(1-b1^t) for Adam, lr/(1-b1^t) for Adamax; device array of ceil(n / batch)).
+ * params / params_t / m / v are updated in place; stats[s * stats_stride + ...] receives the
+ * step's [sum e^2, sum |e|, reg_0 .. reg_{G-1}] (G = ceil(F / 32) workgroups; the regularisation
+ * loss on the pre-update weights is the sum of the reg_g).  exact != 0 runs exact-fp32 MFMA GEMMs.
+ * workspace: hpe_fit_workspace_size bytes; after the launch its int word [1] holds flags
+ * (1: a split accumulator was non-finite — rerun the epoch with exact = 1 from the saved state;
+ * 2: the per-step workgroup exchange timed out).  hpe_fit_supported: 1 if program + batch qualify
+ * (batch <= 512). */
+int hpe_fit_supported(const hpe_program *prog, int32_t batch);
+size_t hpe_fit_workspace_size(const hpe_program *prog, int32_t batch);
+int hpe_fit_epoch(const hpe_program *prog, float *params, float *params_t, float *m, float *v,
+                  const float *l2, const int32_t *tpos, const float *x, const float *y_true,
+                  const int32_t *perm, int64_t n, int32_t batch, int32_t kind, float lr, float beta_1,
+                  float beta_2, float epsilon, const float *alpha, uint64_t seed_base, int64_t iter0,
+                  float *stats, int32_t stats_stride, int32_t exact, void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
  * BlazeFace backbone — replaces the TF call on the fused BlazeFace+regressor
  * graph, `self.model.predict(...)` at BlazePoser/blazeFaceDetectorH5.py:272, for a whole batch.
  * words: the plan hpe/blazeface.py builds from the unified model's model_config (csrc/hpe_prog.h
