@@ -119,6 +119,25 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// lane l <-> lane l ^ 32 in one VALU op (gfx950 v_permlane32_swap) instead of an LDS-pipe bpermute
+__device__ __forceinline__ float xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((__lane_id() & 32) ? r[0] : r[1]);
+}
+
+// wave-wide sum on DPP (VALU: quad_perm, row mirrors, row broadcasts) in a fixed order, the total
+// broadcast from lane 63; a __shfl_xor butterfly is six dependent LDS-pipe round trips instead
+#define DPP_SUM_STEP(v, ctrl, rmask) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rmask, 0xf, false))
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  DPP_SUM_STEP(v, 0xB1, 0xf);   // quad_perm [1,0,3,2]
+  DPP_SUM_STEP(v, 0x4E, 0xf);   // quad_perm [2,3,0,1]
+  DPP_SUM_STEP(v, 0x141, 0xf);  // row_half_mirror
+  DPP_SUM_STEP(v, 0x140, 0xf);  // row_mirror: every lane holds its row's sum
+  DPP_SUM_STEP(v, 0x142, 0xa);  // row_bcast:15 -> rows 1, 3
+  DPP_SUM_STEP(v, 0x143, 0xc);  // row_bcast:31 -> rows 2, 3: lane 63 holds the total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

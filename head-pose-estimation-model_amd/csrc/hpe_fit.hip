@@ -34,7 +34,8 @@
 #define FIT_MAX_BATCH 256      // batch rows (<= 2 tiles per wave: X stays in LDS across the exchange)
 #define FIT_UNION 9216         // floats: A1 park | head-partial table [G][batch][3] | dW1 reduce
 #define FIT_POLL 24            // granules in flight per thread in the exchange
-#define FIT_PART_OFF 16        // workspace (floats): [1] flags, [16..] head-partial granules
+#define FIT_PART_OFF 128       // workspace (words): [1] flags, [2..3] debug, [4..4+G) XCC ids, [128..] granules
+#define FIT_XCC_OFF 4
 
 enum { FIT_FLAG_NONFINITE = 1, FIT_FLAG_TIMEOUT = 2 };
 
@@ -103,22 +104,30 @@ __device__ __forceinline__ bool fit_ok(int64_t i, int64_t bound, int code, int* 
 #define FIT_OK(i, bound, code) true
 #endif
 
-__device__ __forceinline__ void put_granule(uint64_t* p, float v, uint32_t tag) {
-  __hip_atomic_store(p, ((uint64_t)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// same_xcd: every workgroup of the launch sits on one XCD (checked at launch start), whose L2 they
+// share: a plain store stays in that L2, where the readers' sc1 loads (which bypass only L1) hit it;
+// otherwise write-through sc1 stores (visible to every XCD through memory)
+__device__ __forceinline__ void put_granule(uint64_t* p, float v, uint32_t tag, bool same_xcd) {
+  const uint64_t g = ((uint64_t)tag << 32) | __float_as_uint(v);
+  if (same_xcd)
+    __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t get_granule(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// block sum of 5 values (fixed order), scratch: 32 floats
+// block sum of 5 values (fixed order), scratch: 32 floats; LDS-only barriers (the step's
+// write-through partial stores need not drain here)
 __device__ __forceinline__ void bsum5(float (&v)[5], float* scratch) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) v[k] = wave_sum(v[k]);
-  __syncthreads();
+  for (int k = 0; k < 5; ++k) v[k] = wave_sum_dpp(v[k]);
+  bar_lds();
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
     for (int k = 0; k < 5; ++k) scratch[(threadIdx.x >> 6) * 8 + k] = v[k];
-  __syncthreads();
+  bar_lds();
 #pragma unroll
   for (int k = 0; k < 5; ++k) v[k] = (scratch[k] + scratch[8 + k]) + (scratch[16 + k] + scratch[24 + k]);
 }
@@ -142,17 +151,24 @@ __device__ __forceinline__ void opt_update(int kind, float alpha, float lr, floa
 // stage the 32 rows [r0, r0 + 32) of the current batch (clamped to the batch) into an X tile:
 // one LDS-DMA dwordx4 per row with Cin/4 lanes active; the source rows come from the epoch
 // permutation (lane l looks up row l once)
-__device__ __forceinline__ void fit_stage(const FitArgs& a, float* xt, const int* bperm, int r0, int nb, int Cin,
-                                          int lane) {
-  const int lr = min(r0 + (lane & 31), nb - 1);
-  const int src = FIT_OK(bperm - a.perm + lr, a.n, 1) ? bperm[lr] : 0;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the index load, visibly to the compiler
+__device__ __forceinline__ void fit_stage_src(const FitArgs& a, float* xt, int src, int Cin, int lane) {
   const int q = Cin >> 2;
 #pragma unroll 4
   for (int r = 0; r < 32; ++r) {
     const int64_t s = (int64_t)__builtin_amdgcn_readlane(src, r);
     if (lane < q && FIT_OK(s, a.n, 2)) glds16(a.x + s * Cin + 4 * lane, lds_addr(xt + r * FIT_XS));
   }
+}
+// source row of tile row (lane & 31) of the tile at batch row r0 (clamped to the batch)
+__device__ __forceinline__ int fit_src(const FitArgs& a, const int* bperm, int r0, int nb, int lane) {
+  const int lr = min(r0 + (lane & 31), nb - 1);
+  return FIT_OK(bperm - a.perm + lr, a.n, 1) ? bperm[lr] : 0;
+}
+__device__ __forceinline__ void fit_stage(const FitArgs& a, float* xt, const int* bperm, int r0, int nb, int Cin,
+                                          int lane) {
+  const int src = fit_src(a, bperm, r0, nb, lane);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the index load, visibly to the compiler
+  fit_stage_src(a, xt, src, Cin, lane);
 }
 
 template <int KH, int ACT1, bool SPLIT>
@@ -165,7 +181,10 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
   const uint32_t thr1 = (uint32_t)o[O_ETHR], thr2 = (uint32_t)o[O_TCOUNT];
   const float keep1 = __int_as_float(o[O_EKEEP]), keep2 = __int_as_float(o[O_F0]);
   const float inv_keep1 = 1.f / keep1;
-  const int G = gridDim.x, c = blockIdx.x;
+  // the grid is 8 G workgroups of which those with blockIdx % 8 == 0 work: under the round-robin
+  // dispatch over the 8 XCDs they share one XCD (speed only: verified below, never assumed)
+  if (blockIdx.x & 7) return;
+  const int G = gridDim.x >> 3, c = blockIdx.x >> 3;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, half = lane >> 5, l32 = lane & 31;
   const int n = c * 32 + l32;  // this lane's hidden unit (forward / backward)
   const bool nok = n < F;
@@ -235,12 +254,28 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
   }
   __syncthreads();
 
+  // one-time placement check: every workgroup publishes its XCC id; same_xcd iff all are equal
+  if (tid == 0) {
+    const int xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(HW_REG_XCC_ID, 0, 4)
+    __hip_atomic_store(a.sync + FIT_XCC_OFF + c, xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int same = 1;
+    for (int cc = 0; cc < G; ++cc) {
+      int v, it = 0;
+      while ((v = __hip_atomic_load(a.sync + FIT_XCC_OFF + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 &&
+             ++it < (1 << 22))
+        __builtin_amdgcn_s_sleep(1);
+      same &= v == xcc + 1;
+    }
+    misc[41] = same ? 1.f : 0.f;
+  }
+  __syncthreads();
+  const bool same_xcd = misc[41] != 0.f;
   bool bad = false;
   int flags = 0;
   float alpha = a.alpha[0];  // (steps >= 1)  // the next step's is loaded one step ahead
   const bool onetile = a.bs <= 32 * FIT_NW;  // every step: at most one tile per wave
 #ifdef FIT_STAMPS
-  uint64_t ph[8] = {};
+  uint64_t ph[10] = {};
   uint64_t tprev = __builtin_amdgcn_s_memtime();
 #define FSTAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[i] += t_ - tprev; tprev = t_; } while (0)
 #else
@@ -273,7 +308,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
           v[q][j] = (8 * q + j < KH && k < 96) ? w1t[k * 32 + l32] : 0.f;
           mx = fmaxf(mx, fabsf(v[q][j]));
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = fmaxf(mx, xor32(mx));
       const float s1 = pow2_scale(mx, 13);
       inv1 = SPLIT_INV_C / s1;
 #pragma unroll
@@ -326,6 +361,11 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     };
 
     const float alpha_next = FIT_OK(min(s + 1, a.steps - 1), a.steps, 5) ? a.alpha[min(s + 1, a.steps - 1)] : 0.f;
+    // the next step's tile sources (one tile per wave), loaded before this step's partial stores so
+    // the prefetch below never waits for those write-through stores to drain
+    const int nb1 = min(a.bs, a.n - b0 - a.bs);
+    const bool pf = onetile && s + 1 < a.steps && wave < (nb1 + 31) / 32;
+    const int pf_src = pf ? fit_src(a, bperm + a.bs, 32 * wave, nb1, lane) : 0;
     FSTAMP(0);
     // ---- pass 1: forward of this wave's tiles + this workgroup's head partials ----
     // one tile per wave (batch <= 128, the reference's): X tiles alternate slots by step parity and
@@ -364,14 +404,14 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
         p1 = fmaf(av, w.y, p1);
         p2 = fmaf(av, w.z, p2);
       }
-      p0 += __shfl_xor(p0, 32, 64);
-      p1 += __shfl_xor(p1, 32, 64);
-      p2 += __shfl_xor(p2, 32, 64);
+      p0 += xor32(p0);
+      p1 += xor32(p1);
+      p2 += xor32(p2);
       const int R = 32 * t + r;
       if (half == 0 && R < nb && FIT_OK((part_out - a.part) + 2 * a.bs + R, a.n_ws_granules, 6)) {
-        put_granule(part_out + R, p0, tag);
-        put_granule(part_out + a.bs + R, p1, tag);
-        put_granule(part_out + 2 * a.bs + R, p2, tag);
+        put_granule(part_out + R, p0, tag, same_xcd);
+        put_granule(part_out + a.bs + R, p1, tag, same_xcd);
+        put_granule(part_out + 2 * a.bs + R, p2, tag, same_xcd);
       }
       __builtin_amdgcn_wave_barrier();  // a1p reuse by the next tile
     }
@@ -383,9 +423,14 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     float red5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // sse, sae, db2[3]
     // this thread's row label (batch <= 256 = threads: at most one row each), loaded now so its two
     // dependent global reads overlap the exchange
+    // rows <= 128: two threads per row (lane pairs l, l ^ 32 of wave r / 32), each summing every
+    // other workgroup's partials below; the halves meet in fixed order (even c + odd c), so every
+    // workgroup gets the same p
+    const bool pair = ntile * 32 * 2 <= FIT_NW * 64;
+    const int rr = pair ? ((tid >> 6) << 5) + (tid & 31) : tid;
     float ylab[3] = {0.f, 0.f, 0.f};
-    if (tid < nb) {
-      const int src = FIT_OK(bperm - a.perm + tid, a.n, 8) ? bperm[tid] : 0;
+    if (rr < nb) {
+      const int src = FIT_OK(bperm - a.perm + rr, a.n, 8) ? bperm[rr] : 0;
       if (FIT_OK(src, a.n, 9)) {
         ylab[0] = a.ytrue[(int64_t)src * 3 + 0];
         ylab[1] = a.ytrue[(int64_t)src * 3 + 1];
@@ -436,18 +481,31 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
       }
     }
     if (flags & FIT_FLAG_TIMEOUT) misc[40] = 1.f;
+    FSTAMP(8);
     bar_lds();
+    FSTAMP(9);
     if (misc[40] != 0.f) { flags |= FIT_FLAG_TIMEOUT; break; }
-    for (int r = tid; r < ntile * 32; r += blockDim.x) {
+    const int cpar = pair ? half : 0, cstep = pair ? 2 : 1;
+    for (int r = rr; r < ntile * 32 && (!pair || r < 128); r += blockDim.x) {
       f32x4 d = {0.f, 0.f, 0.f, 0.f};
-      if (r < nb) {
-        float p[3] = {b2t[0], b2t[1], b2t[2]};
-        for (int cc = 0; cc < G; ++cc) {
+      {
+        float p[3] = {0.f, 0.f, 0.f};
+        for (int cc = cpar; cc < G; cc += cstep) {
           const float* q = ptab + cc * 3 * a.bs + r;
           p[0] += q[0];
           p[1] += q[a.bs];
           p[2] += q[2 * a.bs];
         }
+        if (pair) {
+          const float o0 = xor32(p[0]), o1 = xor32(p[1]), o2 = xor32(p[2]);
+          p[0] = half ? o0 + p[0] : p[0] + o0;
+          p[1] = half ? o1 + p[1] : p[1] + o1;
+          p[2] = half ? o2 + p[2] : p[2] + o2;
+        }
+        p[0] += b2t[0];
+        p[1] += b2t[1];
+        p[2] += b2t[2];
+        if (r < nb && (!pair || half == 0)) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           float pj = act_f(act2, p[j]);
@@ -465,8 +523,9 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
           d[j] = gj;
           red5[2 + j] += gj;
         }
+        }
       }
-      *(f32x4*)(dz2 + r * 4) = d;
+      if (!pair || half == 0) *(f32x4*)(dz2 + r * 4) = d;
     }
     FSTAMP(2);
     bsum5(red5, misc);  // its barriers also publish the dz2 table
@@ -476,10 +535,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
       a.stats[(size_t)s * a.stats_stride + 1] = red5[1];
     }
     // prefetch the next step's tile (one tile per wave): lands during this step's backward
-    if (onetile && s + 1 < a.steps) {
-      const int nb1 = min(a.bs, a.n - b0 - a.bs);
-      if (wave < (nb1 + 31) / 32) fit_stage(a, xs + ((s + 1) & 1) * FIT_XT, bperm + a.bs, 32 * wave, nb1, Cin, lane);
-    }
+    if (pf) fit_stage_src(a, xs + ((s + 1) & 1) * FIT_XT, pf_src, Cin, lane);
 
     FSTAMP(3);
     // ---- pass 2: backward of this wave's tiles: dZ1, dW1 (MFMA), dW2, db1 ----
@@ -556,8 +612,8 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
       // dW2 / db1: halves combined, then per-wave partials
       float t2[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
-      const float tb = db1 + __shfl_xor(db1, 32, 64);
+      for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + xor32(dw2[j]);
+      const float tb = db1 + xor32(db1);
       if (half == 0) *(f32x4*)(red + (wave * 32 + l32) * 4) = f32x4{t2[0], t2[1], t2[2], tb};
       bar_lds();
       if (wave >= 2) {
@@ -588,8 +644,18 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       reg = fmaf(l2w * wv[i], wv[i], reg);
-      const float gr = fmaf(gv1[i], gsc, 2.f * l2w * wv[i]);
-      opt_update(a.kind, alpha, alpha, a.b1, a.b2, a.eps, gr, wv[i], om[i], ov[i]);
+      gv1[i] = fmaf(gv1[i], gsc, 2.f * l2w * wv[i]);
+    }
+    // one branch on the optimizer kind for the whole block (straight-line updates inside)
+    if (a.kind == HPE_OPT_ADAM) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) opt_update(HPE_OPT_ADAM, alpha, alpha, a.b1, a.b2, a.eps, gv1[i], wv[i], om[i], ov[i]);
+    } else if (a.kind == HPE_OPT_SGD) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) opt_update(HPE_OPT_SGD, alpha, alpha, a.b1, a.b2, a.eps, gv1[i], wv[i], om[i], ov[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) opt_update(HPE_OPT_ADAMAX, alpha, alpha, a.b1, a.b2, a.eps, gv1[i], wv[i], om[i], ov[i]);
     }
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
@@ -612,7 +678,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
       const float gr = fmaf(graw, inv_count, 2.f * sl2 * sw);
       opt_update(a.kind, alpha, alpha, a.b1, a.b2, a.eps, gr, sw, sm, sv);
     }
-    reg = wave_sum(reg);  // per-wave shares: the host sums stats[s][2:]
+    reg = wave_sum_dpp(reg);  // per-wave shares: the host sums stats[s][2:]
     if (lane == 0 && FIT_OK(2 + 4 * c + wave, a.stats_stride, 11)) a.stats[(size_t)s * a.stats_stride + 2 + 4 * c + wave] = reg;
     // post-update tables for the next step's fragments
     if (sidx >= 0) {
@@ -627,8 +693,8 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
 
 #ifdef FIT_STAMPS
   if (lane == 0 && (c == 0 || c == G - 1))
-    printf("FITSTAMP wg %d wave %d steps %d: frag %lu pass1 %lu poll+dz2 %lu bsum %lu pass2 %lu reduce %lu opt %lu rounds %lu\n",
-           c, wave, a.steps, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7]);
+    printf("FITSTAMP wg %d wave %d steps %d same_xcd %d: frag %lu pass1 %lu poll %lu pollbar %lu dz2 %lu bsum %lu pass2 %lu reduce %lu opt %lu rounds %lu\n",
+           c, wave, a.steps, (int)same_xcd, ph[0], ph[1], ph[8], ph[9], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7]);
 #endif
   // ---- epoch end: parameters, transposed mirror and optimizer state back to global memory ----
 #pragma unroll
@@ -684,7 +750,7 @@ extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
   if (w[H_KIND] != KIND_MLP2 || w[H_MODE] != MODE_TRAIN) return 0;
   const int* o = w + w[H_OPS_OFF];
   if (o[O_AUX3] != 3 || (o[O_K] & 3) || o[O_K] > 96 || o[O_K] < 4) return 0;
-  if (o[O_N] < 1 || (o[O_N] + 31) / 32 > 64) return 0;
+  if (o[O_N] < 1 || (o[O_N] + 31) / 32 > 32) return 0;  // 8 G <= 256 workgroups
   if (!fit_pick(w, true)) return 0;
   const int G = (o[O_N] + 31) / 32;
   return batch >= 1 && batch <= FIT_MAX_BATCH && G * batch * 3 <= FIT_UNION;
@@ -694,7 +760,7 @@ extern "C" size_t hpe_fit_workspace_size(const hpe_program* p, int32_t batch) {
   if (!p) return 0;
   const int* w = hpe_prog_words(p);
   const int G = (w[w[H_OPS_OFF] + O_N] + 31) / 32;
-  return FIT_PART_OFF * sizeof(float) + (size_t)2 * G * batch * 3 * sizeof(uint64_t);
+  return FIT_PART_OFF * sizeof(int) + (size_t)2 * G * batch * 3 * sizeof(uint64_t);
 }
 
 extern "C" int hpe_fit_epoch(const hpe_program* p, float* params, float* params_t, float* m, float* v,
@@ -734,7 +800,7 @@ extern "C" int hpe_fit_epoch(const hpe_program* p, float* params, float* params_
   fit_fn k = fit_pick(w, !exact && !hpe_exact_fp32());
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, FIT_LDS_BYTES) != hipSuccess)
     return hpe_fail(HPE_ERUNTIME, "hpe_fit_epoch: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
-  hipLaunchKernelGGL(k, dim3(G), dim3(FIT_NW * 64), FIT_LDS_BYTES, s, a);
+  hipLaunchKernelGGL(k, dim3(8 * G), dim3(FIT_NW * 64), FIT_LDS_BYTES, s, a);
   if (hipGetLastError() != hipSuccess) return hpe_fail(HPE_ERUNTIME, "hpe_fit_epoch: launch failed");
   return HPE_OK;
 }
