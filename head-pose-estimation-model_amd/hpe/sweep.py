@@ -140,7 +140,7 @@ def run_sweep(spec, gpus, count=None, program=None, run_dir='sweep_runs', seed=0
             rid = uuid.uuid4().hex[:8]
             env = dict(os.environ)
             env.update(extra_env or {})
-            env.update(HIP_VISIBLE_DEVICES=str(g), HPE_RUN_ID=rid, HPE_RUN_DIR=os.path.abspath(run_dir))
+            env.update(HIP_VISIBLE_DEVICES=child_device(g), HPE_RUN_ID=rid, HPE_RUN_DIR=os.path.abspath(run_dir))
             t = dict(combo=combo, params=search.params(combo), run_id=rid, gpu=g, returncode=None,
                      metric=None, start=time.time())
             out = open(os.path.join(run_dir, rid + '.out'), 'w')
@@ -181,18 +181,34 @@ def best_trial(trials, goal='minimize'):
 
 
 def visible_gpus():
-    """GPU indices of this node (device count only: no HIP context is created here)."""
+    """Logical GPU positions 0..n-1 within this process's visible set (device count only: no HIP
+    context is created here).  ``child_device`` turns a position into the child's pin."""
     env = os.environ.get('HIP_VISIBLE_DEVICES') or os.environ.get('ROCR_VISIBLE_DEVICES')
     if env:
-        return [int(x) for x in env.split(',') if x.strip()]
+        return list(range(len([x for x in env.split(',') if x.strip()])))
     import torch
     return list(range(torch.cuda.device_count()))
+
+
+def child_device(pos, environ=None):
+    """HIP_VISIBLE_DEVICES value that pins a child to logical position ``pos`` of the parent's
+    visible set.  HIP counts HIP_VISIBLE_DEVICES inside the ROCR_VISIBLE_DEVICES filter, which the
+    child inherits: with a parent HIP list the child gets that list's entry (index or UUID, kept as
+    text); with only a ROCR filter (e.g. ROCR_VISIBLE_DEVICES=4,5) the child gets the position
+    (0 or 1), never the raw ROCR id."""
+    environ = os.environ if environ is None else environ
+    hip = [x.strip() for x in (environ.get('HIP_VISIBLE_DEVICES') or '').split(',') if x.strip()]
+    if hip:
+        if not 0 <= pos < len(hip):
+            raise ValueError('GPU position %d outside HIP_VISIBLE_DEVICES=%s' % (pos, ','.join(hip)))
+        return hip[pos]
+    return str(pos)
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description='run a sweep.yaml with one trial per GPU')
     ap.add_argument('sweep')
-    ap.add_argument('--gpus', default=None, help='comma-separated GPU indices (default: all visible)')
+    ap.add_argument('--gpus', default=None, help='comma-separated GPU positions within the visible set (default: all visible)')
     ap.add_argument('--count', type=int, default=None)
     ap.add_argument('--run-dir', default='sweep_runs')
     ap.add_argument('--seed', type=int, default=0)

@@ -1,15 +1,28 @@
-"""Turn a scripts/profile.sh run (gpurun_out/prof_*) into committed evidence under profiles/:
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of bench.py
-  profiles/<tag>_traffic.csv        per-kernel FETCH_SIZE / WRITE_SIZE (separate --pmc passes)
-  profiles/traffic.json             HBM bytes per launch of the bench's train / infer kernels,
-                                    read back by bench.py as roofline.traffic
+"""Turn the per-line profiles of scripts/gpu_r02.sh (kernel trace) and scripts/pmc_r02.sh (PMC passes)
+into committed evidence under profiles/.
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half the bytes of a wide
-coalesced 16-B/lane stream -> bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE exact for 16-B stores ->
-1024 * WRITE_SIZE.  Only dispatches of the bench's timed kernels are averaged.
+Every bench line is profiled in its OWN process (``bench.py --only <line>``), so a line's dispatches
+never mix with another line's launches of the same kernel name (the round-1 summariser averaged the
+infer launch together with BlazeFace's small regressor launches).  Within one line, dispatches are
+keyed by (kernel name, grid size) and the line's dominant key is the one with the largest total time.
+
+Inputs (gpurun_out/, merged back by gpurun):
+  prof_<tag>_<line>/**/*kernel_stats.csv        rocprofv3 --kernel-trace --stats
+  prof_<tag>_<line>/**/*kernel_trace.csv        per-dispatch trace (durations keyed by grid)
+  pmc_<tag>_<line>_<pass>/**/*counter_collection.csv   rocprofv3 --pmc, one pass per counter group
+Outputs:
+  profiles/<tag>_<line>_kernel_stats.csv        copy of the stats summary
+  profiles/<tag>_<line>_pmc.csv                 per (kernel, grid): dispatches, mean of every counter
+  profiles/traffic.json                         per line: dominant kernel, avg duration, HBM bytes per
+                                                launch, SQ-derived utilisation; read by bench.py
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM / §PMC): FETCH_SIZE (KiB) reports half the bytes of a
+wide coalesced 16-B/lane stream -> bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is exact for 16-B
+stores -> 1024 * WRITE_SIZE.  SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / SQ_WAIT_* count quad-cycles;
+SQ_VALU_MFMA_BUSY_CYCLES counts cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs.
 """
 import csv
-import re
+import glob
 import json
 import os
 import shutil
@@ -19,68 +32,143 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, 'gpurun_out')
 PROF = os.path.join(ROOT, 'profiles')
+N_SIMD = 256 * 4
 
 
-def counters(path, name):
-    agg = defaultdict(list)
+def _one(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    return hits[-1] if hits else None
+
+
+def short(name):
+    return name.split('(')[0].replace('void ', '')
+
+
+def trace_groups(path):
+    """(kernel, grid) -> list of dispatch durations in ns."""
+    g = defaultdict(list)
     with open(path) as fh:
         for r in csv.DictReader(fh):
-            if r['Counter_Name'] == name:
-                agg[r['Kernel_Name']].append(float(r['Counter_Value']))
-    return agg
+            gx = r.get('Grid_Size_X') or r.get('Grid_Size') or '0'
+            key = (short(r['Kernel_Name']), int(float(gx)))
+            g[key].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+    return g
 
 
-def main(tag):
-    os.makedirs(PROF, exist_ok=True)
-    shutil.copy(os.path.join(OUT, 'prof_trace', 'trace_kernel_stats.csv'),
-                os.path.join(PROF, '%s_kernel_stats.csv' % tag))
-    fetch = counters(os.path.join(OUT, 'prof_fetch', 'fetch_counter_collection.csv'), 'FETCH_SIZE')
-    write = counters(os.path.join(OUT, 'prof_write', 'write_counter_collection.csv'), 'WRITE_SIZE')
-    rows = []
+def counter_groups(path):
+    """(kernel, grid) -> {counter: [value per dispatch]}."""
+    per = defaultdict(lambda: defaultdict(dict))
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            key = (short(r['Kernel_Name']), int(float(r.get('Grid_Size') or 0)))
+            did = r.get('Dispatch_Id') or r.get('Correlation_Id')
+            c = r['Counter_Name']
+            per[key][c][did] = per[key][c].get(did, 0.0) + float(r['Counter_Value'])
+    return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def mean(v):
+    return sum(v) / len(v) if v else 0.0
+
+
+def summarize_line(tag, line):
+    tdir = os.path.join(OUT, 'prof_%s_%s' % (tag, line))
+    stats = _one(os.path.join(tdir, '**', '*kernel_stats.csv'))
+    trace = _one(os.path.join(tdir, '**', '*kernel_trace.csv'))
     res = {}
-    per = {}
-    for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        fb = 2 * 1024 * sum(f) / len(f) if f else 0.0
-        wb = 1024 * sum(w) / len(w) if w else 0.0
-        rows.append((k[:120], len(f), fb, wb, fb + wb))
-        per[k.split('(')[0]] = (fb, wb, len(f))
+    if stats:
+        shutil.copy(stats, os.path.join(PROF, '%s_%s_kernel_stats.csv' % (tag, line)))
+    groups = trace_groups(trace) if trace else {}
+    ctr = defaultdict(dict)
+    for p in sorted(glob.glob(os.path.join(OUT, 'pmc_%s_%s_*' % (tag, line)))):
+        f = _one(os.path.join(p, '**', '*counter_collection.csv'))
+        if not f:
+            continue
+        for key, cs in counter_groups(f).items():
+            for c, vals in cs.items():
+                ctr[key][c] = (len(vals), mean(vals))
+    if ctr:
+        names = sorted({c for v in ctr.values() for c in v})
+        with open(os.path.join(PROF, '%s_%s_pmc.csv' % (tag, line)), 'w') as fh:
+            wr = csv.writer(fh)
+            wr.writerow(['kernel', 'grid', 'dispatches'] + names)
+            for key in sorted(ctr):
+                n = max(v[0] for v in ctr[key].values())
+                wr.writerow([key[0][:140], key[1], n] + ['%.6g' % ctr[key][c][1] if c in ctr[key] else ''
+                                                         for c in names])
+    if not groups:
+        return res
+    if line == 'blazeface':
+        # one forward = every launch of the graph; forwards = dispatches of the stem
+        nfwd = max(1, min(len(v) for k, v in groups.items() if k[0].startswith('bf_stem')))
+        tot_ns = sum(sum(v) for v in groups.values()) / nfwd
+        fb = wb = 0.0
+        for key, cs in ctr.items():
+            if 'FETCH_SIZE' in cs:
+                fb += 2 * 1024 * cs['FETCH_SIZE'][1] * cs['FETCH_SIZE'][0]
+            if 'WRITE_SIZE' in cs:
+                wb += 1024 * cs['WRITE_SIZE'][1] * cs['WRITE_SIZE'][0]
+        res = {'kernel': 'all launches of one forward (bf_* + head GEMMs + regressor programs)',
+               'avg_ns': tot_ns, 'forwards': nfwd}
+        if ctr:
+            res.update({'fetch_bytes': fb / nfwd, 'write_bytes': wb / nfwd, 'hbm_bytes_per_launch': (fb + wb) / nfwd})
+        return res
+    key = max(groups, key=lambda k: sum(groups[k]))
+    d = groups[key]
+    res = {'kernel': key[0], 'grid': key[1], 'dispatches': len(d), 'avg_ns': mean(d),
+           'share_of_line_time': sum(d) / sum(sum(v) for v in groups.values())}
+    cs = ctr.get(key)
+    if cs:
+        if 'FETCH_SIZE' in cs:
+            res['fetch_bytes'] = 2 * 1024 * cs['FETCH_SIZE'][1]
+        if 'WRITE_SIZE' in cs:
+            res['write_bytes'] = 1024 * cs['WRITE_SIZE'][1]
+        if 'fetch_bytes' in res and 'write_bytes' in res:
+            res['hbm_bytes_per_launch'] = res['fetch_bytes'] + res['write_bytes']
+        v = {c: x[1] for c, x in cs.items()}
+        if 'GRBM_GUI_ACTIVE' in v:
+            cyc = v['GRBM_GUI_ACTIVE'] / 8.0          # kernel cycles (summed over the 8 XCDs)
+            res['clock_ghz'] = cyc / res['avg_ns'] if res['avg_ns'] else None
+            if 'SQ_VALU_MFMA_BUSY_CYCLES' in v:
+                # fraction of all SIMD-cycles the MFMA pipe was busy
+                res['mfma_busy_frac'] = v['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * N_SIMD)
+        if 'SQ_WAVE_CYCLES' in v and v['SQ_WAVE_CYCLES']:
+            wc = v['SQ_WAVE_CYCLES']
+            for c in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_ACTIVE_INST_VALU',
+                      'SQ_ACTIVE_INST_LDS', 'SQ_WAIT_INST_LDS'):
+                if c in v:
+                    res[c.lower().replace('sq_', '') + '_frac_of_wave_cycles'] = v[c] / wc
+        for c in ('SQ_INSTS_VALU_MFMA_MOPS_F16', 'SQ_INSTS_VALU', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT',
+                  'SQ_INSTS_SALU', 'SQ_INSTS_VMEM'):
+            if c in v:
+                res[c] = v[c]
+    return res
 
-    def put(key, short):
-        fb, wb, _ = per[short]
-        res[key] = {'kernel': short, 'fetch_bytes': fb, 'write_bytes': wb, 'hbm_bytes_per_launch': fb + wb}
 
-    # bench lines -> their dominant kernels (template args: <KH, ACT1, DROP, NWM, SPLIT>; ACT 1 = tanh,
-    # 3 = softsign).  The exact-fp32 instantiations (SPLIT false) are the guarded fallbacks that exit
-    # at once unless the split launch flagged an overflow; the split ones carry the traffic.
-    split = os.environ.get('HPE_EXACT_FP32') != '1'
-    for short in per:
-        if short.startswith('void mlp2_kernel<48') and ', 1, false, 12, %s>' % str(split).lower() in short:
-            put('train', short)
-        elif short.startswith('void mlp2_kernel<44') and ', true, 4, %s>' % str(split).lower() in short:
-            put('train88', short)
-        elif ('chain_split' if split else 'chain_fwd') in short:
-            put('infer', short)
-    # BlazeFace forward = every bf_* launch of one forward (one dispatch each per forward per kernel
-    # name, except the 64x64/32x32 block kernels that run several blocks): bytes per forward
-    bf = [(s, v) for s, v in per.items() if re.match(r'(void )?bf_', s)]
-    if bf:
-        nfwd = min(v[2] for s, v in bf if 'stem' in s) if any('stem' in s for s, _ in bf) else 1
-        tot_f = sum(v[0] * v[2] for _, v in bf) / nfwd
-        tot_w = sum(v[1] * v[2] for _, v in bf) / nfwd
-        res['blazeface'] = {'kernel': 'bf_* (one forward)', 'fetch_bytes': tot_f, 'write_bytes': tot_w,
-                            'hbm_bytes_per_launch': tot_f + tot_w}
-    with open(os.path.join(PROF, '%s_traffic.csv' % tag), 'w') as fh:
-        wr = csv.writer(fh)
-        wr.writerow(['kernel', 'dispatches', 'fetch_bytes_per_launch(x2 gfx950)', 'write_bytes_per_launch', 'hbm_bytes_per_launch'])
-        for r in rows:
-            wr.writerow(r)
-    res['source'] = '%s_traffic.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)' % tag
-    with open(os.path.join(PROF, 'traffic.json'), 'w') as fh:
-        json.dump(res, fh, indent=1)
-    print(json.dumps(res, indent=1))
+def main(tag, lines):
+    os.makedirs(PROF, exist_ok=True)
+    path = os.path.join(PROF, 'traffic.json')
+    out = {}
+    if os.path.exists(path):
+        with open(path) as fh:
+            out = json.load(fh)
+        if out.get('tag') != tag:      # never mix an older round's numbers into this one
+            out = {}
+    for line in lines:
+        r = summarize_line(tag, line)
+        if r:
+            r['source'] = 'profiles/%s_%s_kernel_stats.csv, %s_%s_pmc.csv' % (tag, line, tag, line)
+            out[line] = r
+    out['tag'] = tag
+    out['note'] = ('per bench line, profiled in its own process; FETCH_SIZE x 2 x 1024, WRITE_SIZE x 1024 '
+                   '(gfx950, MI355X_MICROARCH.md); mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / '
+                   '(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)')
+    with open(path, 'w') as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1] if len(sys.argv) > 1 else 'r01')
+    tag = sys.argv[1] if len(sys.argv) > 1 else 'r02'
+    lines = sys.argv[2].split(',') if len(sys.argv) > 2 else ['train', 'infer', 'train88', 'blazeface', 'p1']
+    main(tag, lines)

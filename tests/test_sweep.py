@@ -67,8 +67,10 @@ def test_grid_sweep_two_slots(tmp_path):
 
 def test_bayes_sweep_finds_a_good_region(tmp_path):
     spec = sweep.load_spec(SPEC)
-    trials = sweep.run_sweep(spec, gpus=[0, 1, 2], count=15, program=_fake(tmp_path),
-                             run_dir=str(tmp_path / 'runs'), seed=1, log=lambda *a: None, poll=0.05)
+    # one slot: every proposal sees all earlier results, so the outcome does not depend on which of
+    # several concurrent trials happens to finish first on a loaded host
+    trials = sweep.run_sweep(spec, gpus=[0], count=15, program=_fake(tmp_path),
+                             run_dir=str(tmp_path / 'runs'), seed=1, log=lambda *a: None, poll=0.02)
     assert len({tuple(t['combo']) for t in trials}) == 15       # never repeats while untried remain
     b = sweep.best_trial(trials)
     # 320 combinations, optimum 0.0 at (num_filters 128, dropout 0, l2 0); random 15 rarely gets < 0.02
@@ -111,3 +113,24 @@ def test_gpu_sweep_runs_train96_trials(tmp_path):
     assert all(t['returncode'] == 0 for t in trials), out
     assert all(t['metric'] is not None and np.isfinite(t['metric']) for t in trials)
     assert len(list((tmp_path / 'ck').glob('*.h5'))) == 2
+
+
+def test_child_device_pins_within_the_visible_set():
+    """under ROCR_VISIBLE_DEVICES=4,5 a child must be pinned to position 0 / 1 (HIP counts
+    HIP_VISIBLE_DEVICES inside the inherited ROCR filter), and a parent HIP list (ids or UUIDs) is
+    passed through entry by entry."""
+    assert sweep.child_device(1, {'ROCR_VISIBLE_DEVICES': '4,5'}) == '1'
+    assert sweep.child_device(0, {'HIP_VISIBLE_DEVICES': '6,7'}) == '6'
+    assert sweep.child_device(1, {'HIP_VISIBLE_DEVICES': 'GPU-aa,GPU-bb', 'ROCR_VISIBLE_DEVICES': '2,3'}) == 'GPU-bb'
+    assert sweep.child_device(3, {}) == '3'
+    with pytest.raises(ValueError):
+        sweep.child_device(2, {'HIP_VISIBLE_DEVICES': '6,7'})
+    old = {k: os.environ.pop(k, None) for k in ('HIP_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES')}
+    try:
+        os.environ['ROCR_VISIBLE_DEVICES'] = 'GPU-x,GPU-y,GPU-z'
+        assert sweep.visible_gpus() == [0, 1, 2]
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
