@@ -160,6 +160,8 @@ struct Args {
   uint64_t seed;
   int* guard;        // fp16-split kernels: set to `epoch` when a tile's split overflowed (non-finite)
   int epoch;         //   -> the exact-fp32 kernel of the same launch re-runs (guard == epoch)
+  float* gscr;       // rowprog_kernel<..., GS = true>: per-workgroup slot scratch (H_GSLOTS programs)
+  int pass;          // rowprog_kernel: dW-block pass of a multi-pass (H_NPASS) training program
 };
 
 // ------------------------------------------------------------------------------------------------

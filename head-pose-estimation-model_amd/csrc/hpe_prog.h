@@ -16,6 +16,8 @@ enum {
   H_NPARAMS, H_NPARAMS_TRAIN, H_LDS_FLOATS, H_MAXACC, H_MAXTHIN, H_NTACC, H_OPS_OFF,
   H_SLOTS_OFF, H_BLK_OFF, H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB,
   H_KIND,  // KIND_GENERIC: op list for rowprog_kernel; KIND_MLP2: one OP_MLP2 op for mlp2_kernel
+  H_NPASS,   // generic training programs: launches per step, each owning NW * MAXACC dW blocks (0/1: one)
+  H_GSLOTS,  // generic programs: 1 = tile slots in a per-workgroup device scratch region (too big for LDS)
   H_WORDS = 32
 };
 

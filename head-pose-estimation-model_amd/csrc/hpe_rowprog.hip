@@ -465,9 +465,16 @@ __device__ __forceinline__ void op_lnb(const Ctx& c, const int* o) {
 // ------------------------------------------------------------------------------------------------
 
 
-template <int NW, int MAXACC>
+// GS (global slots): programs whose slot plan exceeds 160 KiB of LDS (the widest residual stacks of
+// the reference, e.g. s25l3n04's 512-256-256-... Conv2D stack, H_GSLOTS) keep their tile slots in a
+// per-workgroup region of a device scratch buffer instead; the interpreter is unchanged (all slot
+// accesses go through c.lds; workgroup-scope barriers order them: one CU, one L1).  Programs with
+// more dW blocks than NW * MAXACC accumulators run H_NPASS launches, pass p owning blocks
+// [p NW MAXACC, (p+1) NW MAXACC) (the forward / backward is recomputed per pass; every other slab
+// entry is written with identical values by each pass).
+template <int NW, int MAXACC, bool GS>
 __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds_[];
   constexpr int NT = NW * 64;
   const int* prog = args.prog;
   const int T = prog[H_T];
@@ -479,6 +486,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
   const int in_slot = prog[H_IN_SLOT], out_slot = prog[H_OUT_SLOT];
   const int Cin = prog[H_CIN], Cout = prog[H_COUT];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  float* lds = GS ? args.gscr + (size_t)blockIdx.x * lds_floats : lds_;
 
   Ctx c;
   c.prog = prog;
@@ -503,7 +511,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
 
   const int in_off = slot_w(c, in_slot, S_OFF), in_st = slot_w(c, in_slot, S_STRIDE);
   const int64_t ntiles = (args.nrows + T - 1) / T;
-  const int* blk = prog + prog[H_BLK_OFF] + wave * MAXACC;
+  const int* blk = prog + prog[H_BLK_OFF] + (args.pass * NW + wave) * MAXACC;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     c.row0 = tile * T;
@@ -659,7 +667,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     }
   }
   // block reduction of the loss sums (fixed order)
-  float* red = lds + lds_floats;  // 2 x NW floats past the program's LDS (all LDS in one array)
+  float* red = GS ? lds_ : lds + lds_floats;  // 2 x NW floats past the program's LDS
   const float a = wave_sum(sse), b = wave_sum(sae);
   __syncthreads();
   if (lane == 0) { red[wave] = a; red[NW + wave] = b; }
@@ -773,6 +781,7 @@ struct hpe_program {
   int grid_cap;
   int64_t n_words;
   mutable int epoch;  // guarded (fp16-split) launches: guard word = dwords[n_words]
+  float* gscr;        // H_GSLOTS programs: grid_cap x H_LDS_FLOATS slot scratch
 };
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
@@ -797,23 +806,28 @@ extern "C" int hpe_set_exact_fp32(int on) {
 
 typedef void (*kfn_t)(Args);
 
-template <int NW>
+template <int NW, bool GS>
 static kfn_t pick_acc(int maxacc) {
-  if (maxacc <= 1) return rowprog_kernel<NW, 1>;
-  if (maxacc <= 2) return rowprog_kernel<NW, 2>;
-  if (maxacc <= 4) return rowprog_kernel<NW, 4>;
-  if (maxacc <= 8) return rowprog_kernel<NW, 8>;
+  if (maxacc <= 1) return rowprog_kernel<NW, 1, GS>;
+  if (maxacc <= 2) return rowprog_kernel<NW, 2, GS>;
+  if (maxacc <= 4) return rowprog_kernel<NW, 4, GS>;
+  if (maxacc <= 8) return rowprog_kernel<NW, 8, GS>;
   return nullptr;
 }
 
-static kfn_t pick_kernel(int nw, int maxacc) {
+static kfn_t pick_kernel(int nw, int maxacc, int gs) {
+  if (gs) return nw == 16 ? pick_acc<16, true>(maxacc) : nullptr;   // global-slot programs: 16 waves
   switch (nw) {
-    case 4: return pick_acc<4>(maxacc);
-    case 8: return pick_acc<8>(maxacc);
-    case 12: return pick_acc<12>(maxacc);
-    case 16: return pick_acc<16>(maxacc);
+    case 4: return pick_acc<4, false>(maxacc);
+    case 8: return pick_acc<8, false>(maxacc);
+    case 12: return pick_acc<12, false>(maxacc);
+    case 16: return pick_acc<16, false>(maxacc);
     default: return nullptr;
   }
+}
+
+static int lds_bytes_of(const int* hdr) {
+  return hdr[H_GSLOTS] ? 64 * 4 : (hdr[H_LDS_FLOATS] + 32) * 4;
 }
 
 extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_program** out) {
@@ -826,15 +840,20 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   if (fused && !mlp2_supported(words)) return fail(HPE_EINVAL, "program: unsupported fused 2-layer geometry");
   if (kind == KIND_CHAIN && (!chain_supported(words) || words[H_MODE] != MODE_FWD))
     return fail(HPE_EINVAL, "program: unsupported fused chain geometry");
-  if (kind == KIND_GENERIC && !pick_kernel(nw, words[H_MAXACC])) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d", nw, words[H_MAXACC]);
+  const int gs = words[H_GSLOTS];
+  if (kind == KIND_GENERIC && !pick_kernel(nw, words[H_MAXACC], gs)) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d GSLOTS=%d", nw, words[H_MAXACC], gs);
+  if (gs && kind != KIND_GENERIC) return fail(HPE_EINVAL, "program: global slots are for generic programs only");
+  if (words[H_NPASS] < 0 || words[H_NPASS] > 64 || (words[H_NPASS] > 1 && words[H_MODE] != MODE_TRAIN))
+    return fail(HPE_EINVAL, "program: NPASS=%d (multi-pass programs are training programs, <= 64 passes)", words[H_NPASS]);
   if (words[H_MAXTHIN] > MAXTHIN) return fail(HPE_EINVAL, "program: MAXTHIN=%d > %d", words[H_MAXTHIN], MAXTHIN);
-  if ((int64_t)(words[H_LDS_FLOATS] + 32) * 4 > 160 * 1024) return fail(HPE_EINVAL, "program: LDS %d floats exceeds 160 KiB", words[H_LDS_FLOATS]);
+  if (!gs && (int64_t)(words[H_LDS_FLOATS] + 32) * 4 > 160 * 1024) return fail(HPE_EINVAL, "program: LDS %d floats exceeds 160 KiB", words[H_LDS_FLOATS]);
   hpe_program* p = new hpe_program();
   memcpy(p->hdr, words, sizeof(p->hdr));
   p->words = new int[n_words];
   memcpy(p->words, words, n_words * sizeof(int32_t));
   p->n_words = n_words;
   p->epoch = 0;
+  p->gscr = nullptr;
   hipError_t e = hipMalloc(&p->dwords, (n_words + 1) * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
   e = hipMemset(p->dwords + n_words, 0, sizeof(int32_t));
@@ -845,7 +864,7 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   int ncu = 256;
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   p->n_cu = ncu;
-  const int lds_bytes = (words[H_LDS_FLOATS] + 32) * 4;
+  const int lds_bytes = gs ? (160 * 1024) / 2 : (words[H_LDS_FLOATS] + 32) * 4;   // GS: 2 x 16 waves per CU
   int per_cu = (160 * 1024) / (lds_bytes > 0 ? lds_bytes : 1);
   const int by_waves = 32 / nw;
   if (per_cu > by_waves) per_cu = by_waves;
@@ -857,8 +876,15 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   } else if (kind == KIND_CHAIN) {
     p->grid_cap = chain_grid_cap(ncu);
   } else {
-    kfn_t k = pick_kernel(nw, words[H_MAXACC]);
-    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (words[H_LDS_FLOATS] + 32) * 4);
+    kfn_t k = pick_kernel(nw, words[H_MAXACC], gs);
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes_of(words));
+    if (gs) {
+      e = hipMalloc(&p->gscr, (size_t)p->grid_cap * words[H_LDS_FLOATS] * sizeof(float));
+      if (e != hipSuccess) {
+        hipFree(p->dwords); delete[] p->words; delete p;
+        return fail(HPE_ERUNTIME, "hipMalloc(global slots): %s", hipGetErrorString(e));
+      }
+    }
   }
   *out = p;
   return HPE_OK;
@@ -867,6 +893,7 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
 extern "C" int hpe_program_destroy(hpe_program* p) {
   if (!p) return HPE_OK;
   hipFree(p->dwords);
+  if (p->gscr) hipFree(p->gscr);
   delete[] p->words;
   delete p;
   return HPE_OK;
@@ -898,9 +925,14 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
     if (chain_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "chain launch: %s", hipGetErrorString(hipGetLastError()));
     return HPE_OK;
   }
-  kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC]);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), (p->hdr[H_LDS_FLOATS] + 32) * 4, s, a);
-  HIPCHK(hipGetLastError());
+  kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC], p->hdr[H_GSLOTS]);
+  a.gscr = p->gscr;
+  const int npass = p->hdr[H_MODE] == MODE_TRAIN && p->hdr[H_NPASS] > 1 ? p->hdr[H_NPASS] : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+    a.pass = pass;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
+    HIPCHK(hipGetLastError());
+  }
   return HPE_OK;
 }
 

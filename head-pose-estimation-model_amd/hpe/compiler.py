@@ -22,7 +22,7 @@ import numpy as np
 HPE_MAGIC = 0x31455048
 (H_MAGIC, H_NOPS, H_NSLOTS, H_T, H_NW, H_IN_SLOT, H_OUT_SLOT, H_CIN, H_COUT, H_NPARAMS,
  H_NPARAMS_TRAIN, H_LDS_FLOATS, H_MAXACC, H_MAXTHIN, H_NTACC, H_OPS_OFF, H_SLOTS_OFF, H_BLK_OFF,
- H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB, H_KIND) = range(25)
+ H_TACC_OFF, H_MODE, H_WG_PER_CU, H_SCRATCH_OFF, H_NTHIN, H_SLAB, H_KIND, H_NPASS, H_GSLOTS) = range(27)
 H_WORDS = 32
 MODE_FWD, MODE_TRAIN, MODE_EVAL = 0, 1, 2
 S_WORDS = 4
@@ -42,6 +42,8 @@ MAXTHIN = 4
 ACC_VARIANTS = (1, 2, 4, 8)
 NW_VARIANTS = (4, 8, 12, 16)
 LDS_LIMIT_FLOATS = 160 * 1024 // 4 - 32
+GS_NW = 16             # global-slot programs (slot plan > LDS) run the 16-wave kernel
+GS_T = 32
 
 
 def _f2i(x):
@@ -761,14 +763,21 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
         score = (acc * nw - ndw if ndw else 0, -nw)
         if best is None or score < best[0]:
             best = (score, nw, acc)
+    npass = 1
     if best is None:
-        raise ValueError('model too large for the row kernel: %d dW blocks, %d thin elements'
-                         % (ndw, nthin))
+        # more dW blocks than one launch's register accumulators: H_NPASS launches per step, each
+        # recomputing the tile's forward / backward and owning NW * 8 blocks
+        nw = max(cand_nw)
+        if -(-nthin // (nw * 64)) > MAXTHIN or nw != max(NW_VARIANTS):
+            raise ValueError('model too large for the row kernel: %d dW blocks, %d thin elements'
+                             % (ndw, nthin))
+        acc = ACC_VARIANTS[-1]
+        npass = -(-ndw // (nw * acc))
+        best = (None, nw, acc)
     _, nw, acc = best
     if NW is None and not training:
         nw, acc = 4, 1
     nt = nw * 64
-
     # slot layout: live intervals over the op list, first-fit in LDS (every writer re-zeroes a
     # slot's padding columns, so regions can be shared by slots that are never live together)
     live = _liveness(E, x_t.slot, y_t.slot, mode)
@@ -800,13 +809,29 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
         return offs, scratch_offs, top
     cands = [T] if T else [128, 64, 32]
     chosen = None
+    gslots = 0
     for Tv in cands:
         offs, scratch, tot = plan(Tv)
         if tot <= LDS_LIMIT_FLOATS:
             chosen = (Tv, offs, scratch, tot)
             break
     if chosen is None:
-        raise ValueError('row program does not fit LDS even at T=%d' % cands[-1])
+        # the slot plan does not fit 160 KiB even at the smallest tile: keep the slots in a
+        # per-workgroup device scratch region (H_GSLOTS; same interpreter, L2/MALL-resident)
+        if NW is not None and NW != GS_NW:
+            raise ValueError('row program does not fit LDS even at T=%d' % cands[-1])
+        gslots = 1
+        if nw != GS_NW:
+            nw = GS_NW
+            nt = nw * 64
+            if ndw:
+                acc = next(a for a in ACC_VARIANTS if a >= min(-(-ndw // nw), ACC_VARIANTS[-1]))
+                npass = -(-ndw // (nw * acc))
+            else:
+                acc = 1
+        Tv = T or GS_T
+        offs, scratch, tot = plan(Tv)
+        chosen = (Tv, offs, scratch, tot)
     Tv, offs, scratch_offs, tot = chosen
     for j, d in enumerate(E.ops):
         if d[O_TYPE] == OP_TDENSE:
@@ -822,10 +847,11 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
     ops_w = []
     for d in E.ops:
         ops_w += [int(d[k]) for k in range(O_WORDS)]
-    blk = [-1] * (nw * acc)
+    blk = [-1] * (npass * nw * acc)
     for j, (iop, kb, nb) in enumerate(dw_blocks):
-        w_, s_ = j % nw, j // nw
-        blk[w_ * acc + s_] = (iop << 16) | (kb << 8) | nb
+        pa, jj = divmod(j, nw * acc)
+        w_, s_ = jj % nw, jj // nw
+        blk[(pa * nw + w_) * acc + s_] = (iop << 16) | (kb << 8) | nb
     n_params = n_train + b.const_off
     hdr[H_MAGIC] = HPE_MAGIC
     hdr[H_NOPS] = len(E.ops)
@@ -851,6 +877,8 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
     hdr[H_SCRATCH_OFF] = scratch
     hdr[H_NTHIN] = nthin
     hdr[H_SLAB] = -(-(n_train + 4) // 4) * 4
+    hdr[H_NPASS] = npass
+    hdr[H_GSLOTS] = gslots
     words = np.asarray(hdr + slots_w + ops_w + blk + tacc_ops, dtype=np.int64)
     words = ((words + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int32)
 
@@ -874,7 +902,7 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
     prog.T, prog.NW, prog.mode = Tv, nw, mode
     prog.C_in, prog.C_out = x_t.C, y_t.C
     prog.info = {'ops': len(E.ops), 'slots': len(E.slots), 'dw_blocks': ndw, 'thin': nthin,
-                 'maxacc': acc, 'lds_bytes': hdr[H_LDS_FLOATS] * 4}
+                 'maxacc': acc, 'lds_bytes': hdr[H_LDS_FLOATS] * 4, 'npass': npass, 'gslots': gslots}
     return prog
 
 
@@ -1021,6 +1049,8 @@ def _fused_program(b, op, kind, T, nw, mode, n_train, l2c, cin, info):
     hdr[H_OPS_OFF] = H_WORDS
     hdr[H_MODE] = mode
     hdr[H_SLAB] = -(-(n_train + 4) // 4) * 4
+    hdr[H_NPASS] = 1
+    hdr[H_GSLOTS] = 0
     hdr[H_KIND] = kind
     words = np.asarray(hdr + op, dtype=np.int64)
     words = ((words + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int32)

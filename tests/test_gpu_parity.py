@@ -59,6 +59,13 @@ TRAIN_CASES = [
     ('9w31h50k', 'adamax', 77, 2),    # create_model_complex: residual blocks
     ('ker7z9mv', 'adam', 50, 2),      # SE + MHA + LayerNorm head (P=1)
     ('o6e5xpan', 'sgd', 64, 2),       # SeparableConv2D
+    # round 2: the 16 large signatures (generic interpreter beyond one launch's LDS / accumulators)
+    ('3v3lb8ln', 'adam', 64, 2),      # create_model(512): 48 dW blocks, 12 waves
+    ('8equl7wt', 'sgd', 100, 2),      # 512-256-128-3: 208 dW blocks -> 2 passes per step
+    ('66kjr5zw', 'adam', 100, 2),     # 512-256-128 residual + dropout: 3 passes, slots in device scratch
+    ('6togj6se', 'adamax', 77, 2),    # 11-layer residual tanh stack: slots in device scratch
+    ('s25l3n04', 'adam', 128, 2),     # 512-256-256-... residual: 3 passes + device-scratch slots
+    ('rtomubjl', 'adam', 64, 2),      # 128-wide residual stack with Activation layers and dropout
 ]
 
 
