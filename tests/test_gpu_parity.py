@@ -317,3 +317,35 @@ def test_training_trajectory_wide_dropout(F, act, dropout, P):
     for k in g.trainable:
         np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
     assert np.isfinite(hist.history['loss']).all()
+
+
+def test_configs2_biwi_train_88_adam_b512():
+    """BASELINE configs[2]: Model-88 training on the reference's own BIWI_train_features_88.npz
+    (44 rows -> train_test_split(0.2, 42) = 35 train / 9 validation, train_88.py:290-297), the
+    stoqa9pt create_model graph from its checkpoint, legacy Adam lr 2.8e-4, batch 512 (one partial
+    batch per epoch), validation every epoch; weights, loss and val_loss after 20 epochs against the
+    float64 oracle's fit on the same rows (dropout masks by the same counter hash)."""
+    from hpe.data import train_test_split
+    d = np.load(DATA + '/BIWI_train_features_88.npz')
+    x = d['features'].reshape(-1, 1, 1, 88).astype(np.float32)
+    y = d['poses'].reshape(-1, 1, 1, 3)
+    tx, vx, ty, vy = train_test_split(x, y, test_size=0.2, random_state=42)
+    assert (tx.shape[0], vx.shape[0]) == (35, 9)
+    mc, w = fixture('stoqa9pt')
+    hpe.set_seed(3)
+    m = hpe.model_from_config(mc, w)
+    m.compile(optimizer=keras.optimizers.Adam(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    epochs = 20
+    hist = m.fit(tx, ty, batch_size=512, epochs=epochs, validation_data=(vx, vy), shuffle=False, verbose=0)
+    g = K.Graph(mc, w)
+    o = K.LegacyOptimizer('adam', 2.8e-4)
+    vlosses = []
+    for it in range(1, epochs + 1):
+        K.train_step(g, o, tx, ty.reshape(-1, 3), drop_seed=hpe.random.dropout_seed(it))
+        pv = g.forward(vx).detach().numpy().reshape(-1, 3)
+        vlosses.append(float(np.mean((pv - vy.reshape(-1, 3)) ** 2)) + float(g.regularization().item()))
+    got = m.weights_dict()
+    for k in g.trainable:
+        np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
+    np.testing.assert_allclose(hist.history['val_loss'], vlosses, rtol=1e-4)
+    assert np.isfinite(hist.history['loss']).all() and hist.history['loss'][-1] < hist.history['loss'][0]
