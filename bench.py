@@ -17,6 +17,8 @@ Also reported (sub-objects of the one JSON line):
   infer      configs[1]: the selected Model-96 head hrchr82r, batch 256 on 96x96 maps, forward only
   train88    Model-88 create_model on 88x88 maps
   blazeface  configs[4]: unified BlazeFace + both pose heads, batch 1024
+  attn       se_transformer_regr_head (attention_model.py:16-72, checkpoint 12uei1sn: SE + 4-head MHA,
+             key_dim 16) on 16x16x88 BlazeFace-tap maps, batch 1024, forward (VALU attention core)
   cpu_baseline  the oracle's torch-CPU fp32 restatement of the headline step on a bounded sample
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -404,6 +406,53 @@ def bench_blazeface(dev, iters, no_cpu):
     return res
 
 
+ATTN_B = 1024
+ATTN_ID = '12uei1sn'
+
+
+def bench_attn(dev, iters):
+    """se_transformer_regr_head (Model-88/attention_model.py:16-72) on H x W = 16 x 16 maps of 88
+    channels (a BlazeFace re_lu_10 tap per frame), checkpoint 12uei1sn (SE r=8, MultiHeadAttention 4
+    heads x key_dim 16, LayerNorms, feed-forward, 1x1-conv head), batch 1024 images: hpe_se_gate ->
+    program B (q|k|v) -> hpe_mha -> program D.  Roofline of the attention core (the dominant FLOPs:
+    4 P^2 D per head per image, fp32 on the VALU) against the dense fp32 vector peak; the row
+    programs and the SE gate are HBM-bound (algorithmic bytes: every stage's input + output rows)."""
+    from hpe.spatial import SpatialHead
+    gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
+    with open(os.path.join(gdir, ATTN_ID + '.json')) as fh:
+        mc = json.load(fh)['model_config']
+    wts = dict(np.load(os.path.join(gdir, ATTN_ID + '.npz')))
+    sh = SpatialHead(mc, wts, dev)
+    P, Cc = 16 * 16, sh.C
+    H, D = sh.plan.mha['H'], sh.plan.mha['D']
+    x, _ = synth(ATTN_B, 77, dev, P=P, c=Cc)
+    for _ in range(3):
+        y = sh.forward(x, P)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(iters):
+        y = sh.forward(x, P)
+    e1.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / iters
+    ms = e0.elapsed_time(e1) / iters
+    attn_flop = 4.0 * P * P * D * H * ATTN_B
+    qkv_w = sh.qkv.program('fwd', P).prog.C_out
+    rows = ATTN_B * P
+    nbytes = 4 * rows * (Cc * 3 + qkv_w + (Cc + 3 * H * D) + (Cc + H * D) + y.shape[1])
+    return {'workload': 'se_transformer_regr_head (checkpoint %s: SE + MHA %d heads x key_dim %d) forward on '
+                        '16x16x%d maps, batch %d images (attention_model.py:16-72)' % (ATTN_ID, H, D, Cc, ATTN_B),
+            'value': ATTN_B / wall, 'unit': 'images/sec', 'ms_per_batch': wall * 1e3, 'dtype': 'fp32',
+            'roofline': {'bound': 'valu', 'achieved': attn_flop / (ms * 1e-3) / 1e12, 'peak': PEAK_FP32 / 1e12,
+                         'unit': 'TFLOP/s', 'frac': attn_flop / (ms * 1e-3) / PEAK_FP32,
+                         'kernel': 'se_gate_kernel + rowprog (q|k|v) + mha_kernel<16> + rowprog (head), whole forward',
+                         'kernel_ms': ms, 'attn_flop_per_launch': attn_flop,
+                         'hbm_bytes_algorithmic': nbytes, 'hbm_frac': nbytes / (ms * 1e-3) / PEAK_HBM}}
+
+
 def bench_infer(hpe, dev, steps):
     """configs[1]: hrchr82r forward, batch 256 of 96x96 maps."""
     gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
@@ -480,7 +529,8 @@ def parse(argv):
     ap.add_argument('--no-train88', action='store_true')
     ap.add_argument('--no-strong', action='store_true')
     ap.add_argument('--no-p1', action='store_true')
-    ap.add_argument('--only', default='', help='comma list of lines to run (train,strong,p1,infer,train88,blazeface)')
+    ap.add_argument('--no-attn', action='store_true')
+    ap.add_argument('--only', default='', help='comma list of lines to run (train,strong,p1,infer,train88,blazeface,attn)')
     return ap.parse_args(argv)
 
 
@@ -560,6 +610,8 @@ def main(argv=None):
         out['infer'] = bench_infer(hpe, dev, a.steps)
     if rank == 0 and want('train88', a.no_train88):
         out['train88'] = bench_train88(hpe, keras, dev, max(5, min(a.steps, 20)), 2)
+    if rank == 0 and want('attn', a.no_attn):
+        out['attn'] = bench_attn(dev, max(10, a.steps))
     if rank == 0 and want('blazeface', a.no_blaze):
         out['blazeface'] = bench_blazeface(dev, max(10, a.steps), a.no_cpu or world > 1)
     if rank == 0 and world == 1 and want('train') and not a.no_cpu:

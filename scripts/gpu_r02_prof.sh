@@ -20,4 +20,9 @@ if [ "${SEEDS:-0}" != 0 ]; then
   step "seed spread"
   timeout -k 10 600 python3 -u scripts/seed_spread_96.py $SEEDS > gpurun_out/seed_spread.log 2>&1 || exit $?
 fi
+for line in ${LATE_LINES:-attn}; do
+  step "trace $line"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$line -o trace --output-format csv -- \
+    python3 bench.py --only $line --no-cpu --steps 10 --warmup 2 > gpurun_out/prof_${TAG}_$line.log 2>&1 || exit $?
+done
 step done
