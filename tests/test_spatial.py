@@ -80,6 +80,23 @@ def _modelC():
     return m.model_config, m.weights_dict()
 
 
+def assert_fp32_parity(got, ref, mc, w, x):
+    """SURVEY §8(c)'s bound (rtol 1e-5, atol 1e-4), widened only where a plain fp32 evaluation of
+    the same graph (the oracle in torch fp32, K.Graph(dtype=float32)) is itself further than that
+    from the float64 oracle: atol = max(1e-4, 4 x that fp32 error).  The attention heads take a
+    softmax over up to P = 2304 tokens of scores q.k whose fp32 rounding error grows with |q||k|
+    and D (DESIGN.md §Oracle and parity), and LayerNorm divides by a small std afterwards, so the
+    fp32 reference error is the honest floor, measured here rather than asserted."""
+    import torch
+    ref32 = K.Graph(mc, w, dtype=torch.float32).forward(x).detach().numpy()
+    e32 = float(np.abs(ref32.astype(np.float64) - ref).max())
+    atol = max(1e-4, 4.0 * e32)
+    err = np.abs(got.astype(np.float64) - ref)
+    bad = err > atol + 1e-5 * np.abs(ref)
+    assert not bad.any(), ('max err %.3g (fp32 reference error %.3g, atol %.3g) at %d elements'
+                           % (err.max(), e32, atol, int(bad.sum())))
+
+
 def _inputs(n, h, w, c, seed):
     rng = np.random.default_rng(seed)
     return np.maximum(0.0, 0.6 * rng.standard_normal((n, h, w, c)) - 0.3).astype(np.float32)
@@ -123,8 +140,7 @@ def test_gpu_spatial_predict_matches_oracle(rid, hw):
     m = hpe.model_from_config(mc, w)
     got = m.predict(x)
     assert got.shape == ref.shape
-    # fp32 throughout; softmax over up to 256 tokens in fp32 (tolerance stated here)
-    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=2e-4)
+    assert_fp32_parity(got, ref, mc, w, x)
 
 
 @pytest.mark.gpu
@@ -140,7 +156,7 @@ def test_gpu_spatial_large_map_and_p1_consistency():
     x = _inputs(2, 48, 48, c, seed=3)
     ref = K.Graph(mc, w).forward(x).detach().numpy()
     got = hpe.model_from_config(mc, w).predict(x)
-    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=5e-4)
+    assert_fp32_parity(got, ref, mc, w, x)
     x1 = _inputs(64, 1, 1, c, seed=4)
     m = hpe.model_from_config(mc, w)
     row = m.predict(x1).reshape(-1, 3)
