@@ -211,7 +211,8 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
   float* red = hacc + NCB * 256;  // [NCB * 64]
-  _Float16* xfb = (_Float16*)(red + NCB * 64);  // PRE: [3][32][MLP2_FS] ch, cl, h; [2][3][96][MLP2_TS]
+  float* colt = red + NCB * 64;   // [NCB * 32][4]: per hidden unit (inv1, b1, s2, -), re-read per tile
+  _Float16* xfb = (_Float16*)(colt + NCB * 128);  // PRE: [3][32][MLP2_FS] ch, cl, h; [2][3][96][MLP2_TS]
   _Float16* xtb = xfb + 3 * 32 * MLP2_FS;
 
   E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
@@ -257,7 +258,12 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     }
   }
   bool bad = false;
-  const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
+  {
+    // the per-unit scalars live in LDS across the tile loop, not in 3 loop-carried VGPRs (the
+    // 12-wave variant sits at the 168-VGPR budget; in registers they pushed a W1 fragment to scratch)
+    const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
+    if (half == 0) *(f32x4*)(colt + n * 4) = f32x4{inv1, b1, s2, 0.f};
+  }
   // small tables in LDS rather than loop-carried VGPRs (the 12-wave variant is at its budget)
   for (int i = threadIdx.x; i < NCB * 128; i += NT) {
     const int nn = i >> 2, j = i & 3;
@@ -381,9 +387,10 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
           }
         }
       }
+      const f32x4 cs = *(const f32x4*)(colt + n * 4);  // (inv1, b1, s2, -)
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        float z = act1_f<ACT1>(e1.act, SPLIT ? fmaf(acc[g], inv1, b1) : acc[g] + b1);
+        float z = act1_f<ACT1>(e1.act, SPLIT ? fmaf(acc[g], cs.x, cs.y) : acc[g] + cs.y);
         if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
         acc[g] = nok ? z : 0.f;
       }
@@ -476,6 +483,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     // ---- backward: dA1 = dZ2.W2^T, dZ1, dW2, db1 in registers; dW1 += X^T.dZ1 on MFMA ----
     {
       const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
+      const float s2 = colt[n * 4 + 2];
       // dZ1 of accumulator register g (row (g & 3) + 8 (g >> 2) + 4 h), dW2 / db1 on the way
       auto dz_of = [&](int g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
@@ -584,6 +592,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   float* ws = args.ws + (size_t)blockIdx.x * slab;
   const float sc = SPLIT ? args.inv_count : 1.f;  // the split path carries unnormalised gradients
   __syncthreads();
+  const float s2f = colt[n * 4 + 2];
   if (train) {
     float chk = 0.f;
 #pragma unroll
@@ -592,7 +601,7 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (SPLIT ? sc * (SPLIT_INV_C / s2) : sc);
+        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (SPLIT ? sc * (SPLIT_INV_C / s2f) : sc);
       }
     }
     if (SPLIT) bad |= !(fabsf(chk) <= 3.0e38f);
@@ -666,7 +675,7 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64 + ncb * 128;
   lds_bytes = (2 * MLP2_XF + rest) * 4;
   // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
   const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;

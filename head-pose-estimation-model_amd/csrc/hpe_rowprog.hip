@@ -780,7 +780,7 @@ struct hpe_program {
   int n_cu;
   int grid_cap;
   int64_t n_words;
-  mutable int epoch;  // guarded (fp16-split) launches: guard word = dwords[n_words]
+  mutable int epoch;  // guarded (fp16-split) launches: guard word = dwords[n_words + epoch % HPE_GUARD_RING]
   float* gscr;        // H_GSLOTS programs: grid_cap x H_LDS_FLOATS slot scratch
 };
 
@@ -805,6 +805,7 @@ extern "C" int hpe_set_exact_fp32(int on) {
 }
 
 typedef void (*kfn_t)(Args);
+#define HPE_GUARD_RING 16
 
 template <int NW, bool GS>
 static kfn_t pick_acc(int maxacc) {
@@ -854,9 +855,9 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   p->n_words = n_words;
   p->epoch = 0;
   p->gscr = nullptr;
-  hipError_t e = hipMalloc(&p->dwords, (n_words + 1) * sizeof(int32_t));
+  hipError_t e = hipMalloc(&p->dwords, (n_words + HPE_GUARD_RING) * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
-  e = hipMemset(p->dwords + n_words, 0, sizeof(int32_t));
+  e = hipMemset(p->dwords + n_words, 0, HPE_GUARD_RING * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) { hipFree(p->dwords); delete p; return fail(HPE_ERUNTIME, "hipMemcpy: %s", hipGetErrorString(e)); }
   int dev = 0;
@@ -914,9 +915,16 @@ extern "C" size_t hpe_workspace_size(const hpe_program* p, int64_t n_rows) {
 
 static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   const int grid = hpe_launch_grid(p, nrows);
-  a.guard = p->dwords + p->n_words;
-  a.epoch = ++p->epoch;
-  if (a.epoch <= 0) a.epoch = p->epoch = 1;
+  // a ring of guard words indexed by the launch epoch: launches of one program in flight on
+  // different streams (up to HPE_GUARD_RING at once) never share the word their split kernel sets
+  // and their exact kernel reads; the epoch counter is bumped atomically (host threads)
+  int ep = __atomic_add_fetch(&p->epoch, 1, __ATOMIC_RELAXED);
+  if (ep <= 0) {
+    __atomic_store_n(&p->epoch, 1, __ATOMIC_RELAXED);
+    ep = 1;
+  }
+  a.epoch = ep;
+  a.guard = p->dwords + p->n_words + (ep % HPE_GUARD_RING);
   if (p->hdr[H_KIND] == KIND_MLP2) {
     if (mlp2_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "mlp2 launch: %s", hipGetErrorString(hipGetLastError()));
     return HPE_OK;

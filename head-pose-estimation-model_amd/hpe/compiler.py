@@ -14,6 +14,7 @@ the feature map is 1x1 (P == 1), which is how the reference trains and evaluates
 stages are a separate kernel path).
 """
 import math
+import os
 import struct
 
 import numpy as np
@@ -42,6 +43,7 @@ MAXTHIN = 4
 ACC_VARIANTS = (1, 2, 4, 8)
 NW_VARIANTS = (4, 8, 12, 16)
 LDS_LIMIT_FLOATS = 160 * 1024 // 4 - 32
+FWD_NW = int(os.environ.get('HPE_FWD_NW', '16'))   # waves of generic inference programs
 GS_NW = 16             # global-slot programs (slot plan > LDS) run the 16-wave kernel
 GS_T = 32
 
@@ -776,7 +778,9 @@ def _finish(b, x_t, y_t, mode, training, P, T, NW, wg_per_cu, n_train, l2c):
         best = (None, nw, acc)
     _, nw, acc = best
     if NW is None and not training:
-        nw, acc = 4, 1
+        # inference programs: one workgroup per CU is typical (slot plans of 60-150 KiB), so its
+        # waves are the CU's only latency hiding for the per-lane weight loads of OP_DENSE
+        nw, acc = FWD_NW, 1
     nt = nw * 64
     # slot layout: live intervals over the op list, first-fit in LDS (every writer re-zeroes a
     # slot's padding columns, so regions can be shared by slots that are never live together)
