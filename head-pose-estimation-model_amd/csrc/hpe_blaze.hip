@@ -13,8 +13,8 @@
 // tap; fp16-split MFMA, see mfma_split), so the depthwise output never exists in memory; the
 // pointwise weights (W^T, as fp16 hi/lo pairs) sit in LDS and
 // the epilogue adds bias + residual (read back from the staged tile) + ReLU and writes NHWC.
-// fp32 throughout (exact-f32 MFMA): per-op HBM traffic = input + output, the depthwise layers'
-// 1.9 FLOP/B make the chain HBM-bound.
+// fp32 arithmetic throughout (every GEMM as fp16 MFMA products at fp32 accuracy): per-op HBM traffic =
+// input + output, the depthwise layers' 1.9 FLOP/B make the chain HBM-bound.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -71,9 +71,15 @@ __device__ __forceinline__ int xcd_work_id(int nwg) {
 // ------------------------------------------------------------------------------------------------
 // stem: 5x5 s2 conv, TF 'same' on 128x128 (pad 1 top/left, 2 bottom/right), 3 -> 24, ReLU.
 // K = (ky, kx, c) over a 6-row window (row 5 has zero weights) split by rows between the two lane
-// halves (half h: ky = 3h + 0..2), so a lane's LDS offset for step s is base + const(s).
+// halves (half h: ky = 3h + 0..2, 45 k each, padded to 48), so a lane's LDS offset for k is its
+// base + a compile-time constant.  The GEMM runs on fp16 MFMA at fp32 accuracy (the exponent-shifted
+// 3-product split of hpe_common.h, six K-steps of v_mfma_f32_32x32x16_f16 x 3 = 18 MFMAs of 32
+// cycles per 32 positions instead of 45 fp32 v_mfma_f32_32x32x2_f32 of 64): weights scaled per
+// output channel by a power of two (pow2_scale), data = the preprocessed frame, |x| <= 1 in the
+// reference ((x - 0.5) / 0.5, blazeFaceDetectorH5.py:244-269; the split's data range is |x| < 64).
 // ------------------------------------------------------------------------------------------------
 #define STEM_KS 45
+#define STEM_NK 6   // K-steps of 8 k per lane half
 __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* f = a.f;
@@ -87,10 +93,29 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
   const int64_t img = wid / tpi;
   const int oy0 = (wid - (int)img * tpi) * TH;
   const float* P_ = a.params;
-  // weights: W^T padded [32][90] (k = (ky*5 + kx)*3 + c, ky < 6), lane n = l32, its half's 45 k
-  float wr[STEM_KS];
+  // weights: W^T padded [32][90] (k = (ky*5 + kx)*3 + c, ky < 6), lane n = l32, its half's 45 k as
+  // split fragments of K-step s = k-local 8 s .. 8 s + 7, scaled by s1 (max |w| of the channel in
+  // [2^13, 2^14)); z = acc * inv + bias, inv = 1 / (C s1)
+  SplitW wsp[STEM_NK];
+  float inv;
+  {
+    f32x8 v[STEM_NK];
+    float mx = 0.f;
 #pragma unroll
-  for (int s = 0; s < STEM_KS; ++s) wr[s] = P_[f[BFO_PWW] + l32 * 90 + half * STEM_KS + s];
+    for (int s = 0; s < STEM_NK; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = 8 * s + j;
+        v[s][j] = q < STEM_KS ? P_[f[BFO_PWW] + l32 * 90 + half * STEM_KS + q] : 0.f;
+        mx = fmaxf(mx, fabsf(v[s][j]));
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float s1 = pow2_scale(mx, 13);
+    inv = SPLIT_INV_C / s1;
+#pragma unroll
+    for (int s = 0; s < STEM_NK; ++s) wsp[s] = split_w8(v[s] * s1);
+  }
   // image tile: LDS row r <-> image row 2*oy0 - padt + r; a row is W*3 contiguous floats placed at
   // column padl (zeros around), no per-element division
   const int iy0 = oy0 * 2 - f[BFO_PADT];
@@ -124,16 +149,21 @@ __global__ void __launch_bounds__(256) bf_stem_kernel(BfArgs a) {
     const float* t = lds + (oyl * 2 + half * 3) * rowf + ox * 6;
     f32x16 acc = {};
 #pragma unroll
-    for (int s = 0; s < STEM_KS; ++s) {
-      const int kyl = s / 15, kx = (s / 3) % 5, c = s % 3;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(t[kyl * rowf + kx * 3 + c], wr[s], acc, 0, 0, 0);
+    for (int s = 0; s < STEM_NK; ++s) {
+      f32x8 xv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = 8 * s + j;   // compile-time: (ky - 3 half, kx, c) = (q / 15, q / 3 % 5, q % 3)
+        xv[j] = q < STEM_KS ? t[(q / 15) * rowf + ((q / 3) % 5) * 3 + q % 3] : 0.f;
+      }
+      acc = mfma3_dw(split_d8(xv), wsp[s], acc);
     }
     if (l32 < Cout) {
       float* drow = a.dst + ((img * Ho + oy0) * Wo) * Cout + l32;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;   // q = qy * Wo + qx
-        const float v = acc[g] + bias;
+        const float v = fmaf(acc[g], inv, bias);
         drow[q * Cout] = v > 0.f ? v : 0.f;
       }
     }
