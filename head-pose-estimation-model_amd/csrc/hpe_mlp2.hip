@@ -26,6 +26,7 @@
 #define MLP2_XS 100             // LDS row stride of an X tile (floats): conflict-free, 16-B aligned
 #define MLP2_XF (32 * MLP2_XS)  // floats per X tile buffer
 #define MLP2_LAB 128            // floats per label buffer: [32 rows][4] (yaw, pitch, roll, pad)
+#define MLP2_RED 32             // floats of the end-of-launch loss reduction (2 x MLP2_MAXW, rounded up)
 // pre-split X tiles (SPLIT kernels of the 12-wave variant, see presplit_tile): the three fp16
 // fragments of the data side of split_d8 (hpe_common.h): ch = fp16(C x), cl = fp16(C x - ch), h = fp16(x)
 #define MLP2_FS 104             // row stride (halves) of the forward layout [32 rows][2 x 48]: conflict-free b128
@@ -210,8 +211,8 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
   float* w2t = a1s + NCB * 1024;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
-  float* red = hacc + NCB * 256;  // [NCB * 64]
-  float* colt = red + NCB * 64;   // [NCB * 32][4]: per hidden unit (inv1, b1, s2, -), re-read per tile
+  float* red = hacc + NCB * 256;  // [2 * MLP2_MAXW]: block reduction of the loss sums
+  float* colt = red + MLP2_RED;   // [NCB * 32][4]: per hidden unit (inv1, b1, s2, -), re-read per tile
   _Float16* xfb = (_Float16*)(colt + NCB * 128);  // PRE: [3][32][MLP2_FS] ch, cl, h; [2][3][96][MLP2_TS]
   _Float16* xtb = xfb + 3 * 32 * MLP2_FS;
 
@@ -466,7 +467,9 @@ __global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
     STAMP(6);
     if constexpr (PRE) {
       // the next tile landed -> barrier -> split it (forward layout: this tile's forward is done;
-      // transposed: the other parity, this tile's backward reads its own)
+      // transposed: the other parity, this tile's backward reads its own).  Splitting it earlier,
+      // by waves 2.. during the head (after a vmcnt(0) before the second barrier), measured slower
+      // (3.80 -> 3.92 ms, round 2 A/B)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar_lds();
       STAMP(7);
@@ -675,7 +678,7 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + ncb * 64 + ncb * 128;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
   lds_bytes = (2 * MLP2_XF + rest) * 4;
   // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
   const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;
