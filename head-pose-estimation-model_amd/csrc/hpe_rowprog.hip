@@ -61,12 +61,21 @@ __device__ __forceinline__ void op_dense(const Ctx& c, const int* o) {
     const float* bp = W + (size_t)kbase * N + (nok ? n : 0);
     f32x16 acc = {};
     int m = 0;
+    // B (weights, L2-resident) is loaded one 8-k step ahead: its latency hides under the previous
+    // step's 8 MFMAs instead of stalling every step
+    float bn[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bn[j] = (nok && j < kval && 8 <= Kh) ? bp[(size_t)j * N] : 0.f;
     for (; m + 8 <= Kh; m += 8) {
       const f32x4 a0 = *(const f32x4*)(ap + m);
       const f32x4 a1 = *(const f32x4*)(ap + m + 4);
       float b[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) b[j] = (nok && m + j < kval) ? bp[(size_t)(m + j) * N] : 0.f;
+      for (int j = 0; j < 8; ++j) b[j] = bn[j];
+      if (m + 16 <= Kh) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bn[j] = (nok && m + 8 + j < kval) ? bp[(size_t)(m + 8 + j) * N] : 0.f;
+      }
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b[0], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b[1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b[2], acc, 0, 0, 0);
@@ -330,11 +339,18 @@ __device__ __forceinline__ void op_din(const Ctx& c, const int* o) {
     const float* ap = c.lds + a_off + (rb * 32 + l32) * a_st + nbase;
     const float* bp = WT + (size_t)nbase * K + (kok ? k : 0);
     f32x16 acc = {};
+    float bn[4];  // W^T loaded one 4-n step ahead (latency under the previous step's MFMAs)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bn[j] = (kok && j < nval) ? bp[(size_t)j * K] : 0.f;
     for (int m = 0; m < Nh; m += 4) {
       const f32x4 a0 = *(const f32x4*)(ap + m);
       float b[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = (kok && m + j < nval) ? bp[(size_t)(m + j) * K] : 0.f;
+      for (int j = 0; j < 4; ++j) b[j] = bn[j];
+      if (m + 4 < Nh) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bn[j] = (kok && m + 4 + j < nval) ? bp[(size_t)(m + 4 + j) * K] : 0.f;
+      }
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b[0], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b[1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, b[2], acc, 0, 0, 0);

@@ -43,7 +43,7 @@ MAXTHIN = 4
 ACC_VARIANTS = (1, 2, 4, 8)
 NW_VARIANTS = (4, 8, 12, 16)
 LDS_LIMIT_FLOATS = 160 * 1024 // 4 - 32
-FWD_NW = int(os.environ.get('HPE_FWD_NW', '16'))   # waves of generic inference programs
+FWD_NW = int(os.environ.get('HPE_FWD_NW', '8'))   # waves of generic inference programs (16 spills)
 GS_NW = 16             # global-slot programs (slot plan > LDS) run the 16-wave kernel
 GS_T = 32
 
