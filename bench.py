@@ -415,7 +415,7 @@ def bench_attn(dev, iters):
     channels (a BlazeFace re_lu_10 tap per frame), checkpoint 12uei1sn (SE r=8, MultiHeadAttention 4
     heads x key_dim 16, LayerNorms, feed-forward, 1x1-conv head), batch 1024 images: hpe_se_gate ->
     program B (q|k|v) -> hpe_mha -> program D.  Roofline of the attention core (the dominant FLOPs:
-    4 P^2 D per head per image, fp32 on the VALU) against the dense fp32 vector peak; the row
+    4 P^2 D per head per image, exact fp32 MFMA) against the dense fp32 MFMA peak; the row
     programs and the SE gate are HBM-bound (algorithmic bytes: every stage's input + output rows)."""
     from hpe.spatial import SpatialHead
     gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
@@ -446,9 +446,10 @@ def bench_attn(dev, iters):
     return {'workload': 'se_transformer_regr_head (checkpoint %s: SE + MHA %d heads x key_dim %d) forward on '
                         '16x16x%d maps, batch %d images (attention_model.py:16-72)' % (ATTN_ID, H, D, Cc, ATTN_B),
             'value': ATTN_B / wall, 'unit': 'images/sec', 'ms_per_batch': wall * 1e3, 'dtype': 'fp32',
-            'roofline': {'bound': 'valu', 'achieved': attn_flop / (ms * 1e-3) / 1e12, 'peak': PEAK_FP32 / 1e12,
+            'roofline': {'bound': 'mfma', 'achieved': attn_flop / (ms * 1e-3) / 1e12, 'peak': PEAK_FP32 / 1e12,
                          'unit': 'TFLOP/s', 'frac': attn_flop / (ms * 1e-3) / PEAK_FP32,
-                         'kernel': 'se_gate_kernel + rowprog (q|k|v) + mha_kernel<16> + rowprog (head), whole forward',
+                         'kernel': 'se_gate_kernel + rowprog (q|k|v) + mha_mfma_kernel<16> (exact fp32 MFMA) + '
+                                   'rowprog (head), whole forward; peak = dense fp32 MFMA',
                          'kernel_ms': ms, 'attn_flop_per_launch': attn_flop,
                          'hbm_bytes_algorithmic': nbytes, 'hbm_frac': nbytes / (ms * 1e-3) / PEAK_HBM}}
 

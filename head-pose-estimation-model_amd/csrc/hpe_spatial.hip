@@ -19,6 +19,7 @@
 // the 1x1-conv regressor) run as ordinary row programs (hpe/spatial.py builds them).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/hpe.h"
 #include "hpe_common.h"
@@ -195,6 +196,123 @@ __global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ i
     for (int c = 0; c < C; ++c) orow[c] = qrow[c];
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// hpe_mha on fp32 MFMA (key_dim <= 32, every checkpoint but none): flash-style, one wave per 32
+// queries, exact fp32 (v_mfma_f32_32x32x2_f32), keys / values of the head streamed through LDS in
+// blocks of MHAM_KB tokens, 32-key sub-blocks:
+//   S^T[key i][query j] = K_blk . Q^T  (A = K rows from LDS, lane = key; B = Q^T from the wave's
+//                                       registers, lane = query)  -> accumulator: lane = query j,
+//                                       16 registers = keys (g & 3) + 8 (g >> 2) + 4 half
+//   online softmax per query: the 32 scores of a sub-block sit in lanes j and j + 32 (one xor-32
+//   exchange for the max); each lane keeps its own partial exp-sum (combined once at the end)
+//   O^T[d][query j] += V^T . P^T  (B = P^T is the score accumulator itself: MFMA step t takes
+//                                   register t, i.e. key (t & 3) + 8 (t >> 2) + 4 half on half h;
+//                                   A = V^T, lane = d, read from LDS for that same key)
+//   -> O^T accumulator: lane = query j, registers = d rows: the output row of query j, no shuffles.
+// The VALU kernel above remains for key_dim > 32.
+// ------------------------------------------------------------------------------------------------
+#define MHAM_W 4              // waves per workgroup (32 queries each)
+#define MHAM_KB 128           // keys per LDS block
+template <int D>              // key_dim padded to an even number <= 32
+__global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __restrict__ in, int ld_in, int C,
+                                                               float* __restrict__ out, int ld_out, int P, int H,
+                                                               int nqb, int KD) {
+  constexpr int DS = D + 1;   // LDS row stride (odd: the 32 key rows of an A read hit distinct banks)
+  __shared__ float ks[MHAM_KB * DS];
+  __shared__ float vs[MHAM_KB * DS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int qb = blockIdx.x % nqb;
+  const int h = (blockIdx.x / nqb) % H;
+  const int64_t img = blockIdx.x / (nqb * H);
+  const int HD = H * KD;
+  const int64_t row0 = img * P;
+  const int q = qb * (MHAM_W * 32) + wave * 32 + l32;   // this lane's query (both halves)
+  const bool qok = q < P;
+  // Q^T operand of step t: Q[q][2t + half]
+  float qv[D / 2];
+  {
+    const float* qr = in + (row0 + (qok ? q : 0)) * ld_in + C + h * KD;
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t) {
+      const int d = 2 * t + half;
+      qv[t] = (qok && d < KD) ? qr[d] : 0.f;
+    }
+  }
+  f32x16 o = {};
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < P; k0 += MHAM_KB) {
+    const int nk = min(MHAM_KB, P - k0);
+    __syncthreads();  // the previous block's readers are done
+    for (int e = threadIdx.x; e < MHAM_KB * D; e += MHAM_W * 64) {
+      const int j = e / D, d = e - j * D;
+      float kv = 0.f, vv = 0.f;
+      if (j < nk && d < KD) {
+        const float* kr = in + (row0 + k0 + j) * ld_in + C + HD + h * KD;
+        kv = kr[d];
+        vv = kr[HD + d];
+      }
+      ks[j * DS + d] = kv;
+      vs[j * DS + d] = vv;
+    }
+    __syncthreads();
+    for (int j0 = 0; j0 < nk; j0 += 32) {
+      // S^T block: A = K rows j0 + l32 (lane = key), k = 2t + half
+      f32x16 sacc = {};
+      const float* kr = ks + (j0 + l32) * DS + half;
+#pragma unroll
+      for (int t = 0; t < D / 2; ++t) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[2 * t], qv[t], sacc, 0, 0, 0);
+      // keys past the block end: -inf (exp -> 0)
+      float mb = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int key = j0 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        if (key >= nk) sacc[g] = -INFINITY;
+        mb = fmaxf(mb, sacc[g]);
+      }
+      mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+      const float mn = fmaxf(m, mb);
+      const float corr = __expf(m - mn);  // m = -inf on the first sub-block -> 0
+      l *= corr;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) o[g] *= corr;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        sacc[g] = __expf(sacc[g] - mn);
+        l += sacc[g];
+      }
+      m = mn;
+      // O^T += V^T . P^T: step t takes P^T from score register t (key (t&3) + 8(t>>2) + 4 half)
+      const float* vr = vs + j0 * DS + (l32 < D ? l32 : 0);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int key = (t & 3) + 8 * (t >> 2) + 4 * half;
+        const float a = l32 < D ? vr[key * DS] : 0.f;
+        o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, sacc[t], o, 0, 0, 0);
+      }
+    }
+  }
+  // both halves hold partial exp-sums of their keys
+  l += __shfl_xor(l, 32, 64);
+  if (qok) {
+    const float inv = 1.f / l;
+    float* orow = out + (row0 + q) * ld_out + C + h * KD;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int d = (g & 3) + 8 * (g >> 2) + 4 * half;
+      if (d < KD) orow[d] = o[g] * inv;
+    }
+  }
+  // pass-through columns [0, C) of this workgroup's query rows, by head 0 (coalesced)
+  if (h == 0) {
+    const int qa = qb * (MHAM_W * 32), qe = min(qa + MHAM_W * 32, P);
+    for (int e = threadIdx.x; e < (qe - qa) * C; e += MHAM_W * 64) {
+      const int r = e / C, c = e - r * C;
+      out[(row0 + qa + r) * ld_out + c] = in[(row0 + qa + r) * ld_in + c];
+    }
+  }
+}
+
 extern "C" int hpe_se_gate(const float* x, float* xg, int64_t n_images, int32_t P, int32_t C,
                            const float* w1, const float* b1, int32_t U, int32_t act1, const float* w2,
                            const float* b2, int32_t act2, void* stream) {
@@ -226,10 +344,25 @@ extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, in
     return hpe_fail(HPE_EINVAL, "hpe_mha: bad shape P=%d C=%d H=%d D=%d ld_in=%d ld_out=%d", P, C, H, D,
                     ld_in, ld_out);
   if (n_images == 0) return HPE_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (D <= 32 && !getenv("HPE_MHA_VALU")) {
+    const int nqb = (P + MHAM_W * 32 - 1) / (MHAM_W * 32);
+    const int64_t grid = n_images * H * nqb;
+    if (grid > 0x7fffffff) return hpe_fail(HPE_EINVAL, "hpe_mha: grid too large");
+#define MHAM_CASE(DD) \
+    case DD: hipLaunchKernelGGL(mha_mfma_kernel<DD>, dim3((unsigned)grid), dim3(MHAM_W * 64), 0, s, in, ld_in, C, out, ld_out, P, H, nqb, D); break;
+    switch ((D + 1) & ~1) {
+      MHAM_CASE(2) MHAM_CASE(4) MHAM_CASE(6) MHAM_CASE(8) MHAM_CASE(10) MHAM_CASE(12) MHAM_CASE(14) MHAM_CASE(16)
+      MHAM_CASE(18) MHAM_CASE(20) MHAM_CASE(22) MHAM_CASE(24) MHAM_CASE(26) MHAM_CASE(28) MHAM_CASE(30) MHAM_CASE(32)
+      default: return hpe_fail(HPE_EINVAL, "hpe_mha: key_dim %d", D);
+    }
+#undef MHAM_CASE
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HPE_OK : hpe_fail(HPE_ERUNTIME, "hpe_mha: %s", hipGetErrorString(e));
+  }
   const int nqb = (P + MHA_QB - 1) / MHA_QB;
   const int64_t grid = n_images * H * nqb;
   if (grid > 0x7fffffff) return hpe_fail(HPE_EINVAL, "hpe_mha: grid too large");
-  hipStream_t s = (hipStream_t)stream;
 #define MHA_CASE(DD) \
   case DD: hipLaunchKernelGGL(mha_kernel<DD>, dim3((unsigned)grid), dim3(MHA_QB), 0, s, in, ld_in, C, out, ld_out, P, H, nqb, D); break;
   switch ((D + 3) & ~3) {
