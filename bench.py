@@ -289,6 +289,39 @@ def bench_p1(keras, batches=(128, 512), n_rows=1 << 20, epochs=3, no_cpu=False):
             os.environ.pop('HPE_FIT_FUSED', None)
         else:
             os.environ['HPE_FIT_FUSED'] = prev
+    # Model-88 in the reference's own regime on the reference's own training data (train_88.py:
+    # 20-62, 270): create_model 88-64 softsign, dropout 1e-4, l2 1e-6, legacy SGD lr 2.8e-4, batch 128
+    d88 = np.load(os.path.join(ROOT, 'tests', 'golden', 'data', 'BIWI_Train_Enlarged_features_88_0.7_1.npz'))
+    x88 = d88['features'].reshape(-1, 1, 1, 88).astype(np.float32)
+    y88 = d88['poses'].reshape(-1, 1, 1, 3).astype(np.float32)
+    t88x, v88x, t88y, v88y = train_test_split(x88, y88, test_size=0.2, random_state=42)
+    try:
+        for mode in ('per_step', 'fused_epoch'):
+            os.environ['HPE_FIT_FUSED'] = '0' if mode == 'per_step' else '1'
+            hpe.set_seed(42)
+            keras.backend.clear_session()
+            reg = keras.regularizers.l2(1e-6)
+            inp = keras.Input(shape=(None, None, 88))
+            h = keras.layers.Conv2D(64, 1, activation='softsign', kernel_regularizer=reg)(inp)
+            h = keras.layers.SpatialDropout2D(1e-4)(h)
+            o = keras.layers.Conv2D(3, 1, kernel_regularizer=reg)(h)
+            o = keras.layers.SpatialDropout2D(1e-4)(o)
+            m = keras.Model(inp, o)
+            m.compile(optimizer=keras.optimizers.SGD(learning_rate=0.00028), loss='mse', metrics=['mae'])
+            tm = _EpochTimer()
+            m.fit(t88x, t88y, batch_size=128, epochs=21, validation_data=(v88x, v88y), callbacks=[tm], verbose=0)
+            steps = math.ceil(t88x.shape[0] / 128)
+            t_ep = float(np.median(tm.times[1:]))
+            out['lines']['model88_real_%s_b128' % mode] = {
+                'data': 'BIWI_Train_Enlarged_features_88 (10,284 rows, 8,227 train / 2,057 validation)',
+                'us_per_step': t_ep / steps * 1e6, 'images_per_sec': t88x.shape[0] / t_ep, 'epoch_s': t_ep,
+                'steps_per_epoch': steps, 'epochs_timed': len(tm.times) - 1,
+                'fused': bool(getattr(m, '_last_fit_fused', False))}
+    finally:
+        if prev is None:
+            os.environ.pop('HPE_FIT_FUSED', None)
+        else:
+            os.environ['HPE_FIT_FUSED'] = prev
     if not no_cpu:
         sys.path.insert(0, ROOT)
         from oracle import keras_ref as K

@@ -1,0 +1,118 @@
+"""Seed spread of from-scratch Model-88 training against the reference's own checkpoint stoqa9pt
+(PARITY UNPINNED: TF is absent; this compares error distributions, not bits).
+
+stoqa9pt (Model-88/Trained-Models-88/stoqa9pt.h5) is train_88.py's create_model: Conv2D(64, softsign,
+L2 1e-6) -> SpatialDropout2D(1e-4) -> Conv2D(3, L2 1e-6) -> SpatialDropout2D(1e-4), trained with legacy
+SGD lr 2.8e-4 (its training_config) for 770,868 steps (its SGD/iter).  This script repeats
+train_88.py's loop (config :20-62, split / callbacks / fit :256-363): batch 128, 80/20
+train_test_split(random_state=42), EarlyStopping(val_loss, patience 40, min_delta 1e-3,
+restore_best_weights), then evaluate on AFLW2000_Enlarged_features_88 and
+BIWI_Test_Enlarged_features_88, where stoqa9pt scores 7.8100 / 3.4456.  Training data:
+BIWI_Train_Enlarged_features_88 (10,284 rows); the reference also concatenated
+BIWI_NoTrack_Enlarged_features_88, which is absent from the reference checkout.  One run per seed on
+this GPU through Model.fit (fused epoch launches).  Writes gpurun_out/seed_spread_88.json.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'head-pose-estimation-model_amd'))
+DATA = os.path.join(ROOT, 'tests', 'golden', 'data')
+
+
+def create_model(keras):
+    reg = keras.regularizers.l2(1e-6)
+    inp = keras.Input(shape=(None, None, 88))
+    x = keras.layers.Conv2D(64, 1, padding='same', activation='softsign', kernel_regularizer=reg,
+                            kernel_initializer=keras.initializers.GlorotUniform())(inp)
+    x = keras.layers.SpatialDropout2D(1e-4)(x)
+    o = keras.layers.Conv2D(3, 1, padding='same', activation='linear', kernel_regularizer=reg,
+                            kernel_initializer=keras.initializers.GlorotUniform())(x)
+    o = keras.layers.SpatialDropout2D(1e-4)(o)
+    m = keras.Model(inp, o)
+    m.compile(optimizer=keras.optimizers.SGD(learning_rate=0.00028), loss='mse', metrics=['mae'])
+    return m
+
+
+class Progress:
+    """prints a line every `every` epochs (long runs must show progress on the GPU box)"""
+
+    def __init__(self, every=1000):
+        self.every, self.model, self.params, self.t0 = every, None, {}, time.perf_counter()
+
+    def set_model(self, m):
+        self.model = m
+
+    def set_params(self, p):
+        self.params = p
+
+    def on_train_begin(self, logs=None):
+        pass
+
+    def on_train_end(self, logs=None):
+        pass
+
+    def on_epoch_begin(self, epoch, logs=None):
+        pass
+
+    def on_epoch_end(self, epoch, logs=None):
+        if (epoch + 1) % self.every == 0:
+            print('  epoch %d val_loss %.4f (%.1f s)' % (epoch + 1, logs.get('val_loss', float('nan')),
+                                                        time.perf_counter() - self.t0), flush=True)
+
+
+def load(name):
+    d = np.load(os.path.join(DATA, name))
+    return d['features'].reshape(-1, 1, 1, 88).astype(np.float32), d['poses'].reshape(-1, 1, 1, 3)
+
+
+def main(seeds, max_epochs):
+    import hpe
+    from hpe import keras
+    from hpe.data import train_test_split
+    x, y = load('BIWI_Train_Enlarged_features_88_0.7_1.npz')
+    tx, vx, ty, vy = train_test_split(x, y, test_size=0.2, random_state=42)
+    ax, ay = load('AFLW2000_Enlarged_features_88_0.7_1.npz')
+    bx, by = load('BIWI_Test_Enlarged_features_88_0.7_1.npz')
+    runs = []
+    os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+    for s in seeds:
+        hpe.set_seed(s)
+        keras.backend.clear_session()
+        m = create_model(keras)
+        es = keras.callbacks.EarlyStopping(monitor='val_loss', patience=40, min_delta=0.001,
+                                           restore_best_weights=True)
+        t0 = time.perf_counter()
+        h = m.fit(tx, ty, epochs=max_epochs, batch_size=128, validation_data=(vx, vy), callbacks=[es, Progress()], verbose=0)
+        dt = time.perf_counter() - t0
+        _, a_mae = m.evaluate(ax, ay, verbose=0)
+        _, b_mae = m.evaluate(bx, by, verbose=0)
+        ep = len(h.history['loss'])
+        r = {'seed': s, 'epochs': ep, 'steps': ep * -(-tx.shape[0] // 128),
+             'best_epoch': int(np.argmin(h.history['val_loss'])) + 1,
+             'best_val_loss': float(np.min(h.history['val_loss'])), 'aflw2000_enlarged_mae': float(a_mae),
+             'biwi_test_enlarged_mae': float(b_mae), 'fit_seconds': dt,
+             'fused_epochs': bool(getattr(m, '_last_fit_fused', False))}
+        runs.append(r)
+        print(json.dumps(r), flush=True)
+    a = np.array([r['aflw2000_enlarged_mae'] for r in runs])
+    b = np.array([r['biwi_test_enlarged_mae'] for r in runs])
+    out = {'what': 'train_88.py create_model (64 softsign, dropout 1e-4, l2 1e-6), legacy SGD lr 2.8e-4, batch 128, '
+                   'trained from scratch per seed on BIWI_Train_Enlarged_features_88 (BIWI_NoTrack_Enlarged absent); '
+                   'MAE vs the reference checkpoint stoqa9pt -- parity unpinned',
+           'reference_stoqa9pt': {'aflw2000_enlarged_mae': 7.8100, 'biwi_test_enlarged_mae': 3.4456, 'sgd_steps': 770868},
+           'runs': runs, 'max_epochs': max_epochs,
+           'aflw2000_enlarged_mae_mean': float(a.mean()), 'aflw2000_enlarged_mae_std': float(a.std(ddof=1)) if len(a) > 1 else 0.0,
+           'biwi_test_enlarged_mae_mean': float(b.mean()), 'biwi_test_enlarged_mae_std': float(b.std(ddof=1)) if len(b) > 1 else 0.0}
+    with open(os.path.join(ROOT, 'gpurun_out', 'seed_spread_88.json'), 'w') as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != 'runs'}), flush=True)
+
+
+if __name__ == '__main__':
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    main(list(range(n)), int(sys.argv[2]) if len(sys.argv) > 2 else 15000)

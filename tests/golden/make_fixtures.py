@@ -43,7 +43,8 @@ UNIFIED = ['reg1-stoqa9pt-reg2-hrchr82r-selected', 'reg1-stoqa9pt-reg2-cl4obelj'
 DATASETS = ['AFLW2000_features_88_0.7_1.npz', 'AFLW2000_features_96_0.7_1.npz',
             'AFLW2000_Enlarged_features_88_0.7_1.npz', 'BIWI_train_features_88.npz',
             'BIWI_test_features_88.npz', 'BIWI_Test_Enlarged_features_88_0.7_1.npz',
-            'BIWI_Train_Enlarged_features_96_0.7_1.npz', 'BIWI_Test_Enlarged_features_96_0.7_1.npz']
+            'BIWI_Train_Enlarged_features_96_0.7_1.npz', 'BIWI_Test_Enlarged_features_96_0.7_1.npz',
+            'BIWI_Train_Enlarged_features_88_0.7_1.npz']   # Model-88's training set (train_88.py:270)
 
 
 def strip(mc):
