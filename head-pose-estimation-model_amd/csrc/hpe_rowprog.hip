@@ -32,6 +32,24 @@
 #include "hpe_common.h"
 
 
+
+// the (row, column) items of a T x C block over NT threads: thread t takes column t % C and rows
+// t / C, t / C + NT / C, ... (one division per thread and op instead of one per item)
+template <int NT, typename F>
+__device__ __forceinline__ void for_rc(int T, int C, F&& f) {
+  if (C <= 0) return;
+  if (C <= NT) {
+    const int rs = NT / C, r0 = (int)threadIdx.x / C, ch = (int)threadIdx.x - r0 * C;
+    if (r0 < rs)
+      for (int r = r0; r < T; r += rs) f(r, ch);
+  } else {
+    for (int it = threadIdx.x; it < T * C; it += NT) {
+      const int r = it / C;
+      f(r, it - r * C);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // OP_DENSE: out[r][n] = epi(sum_k a[r][k] W[k][n] + b[n]) on fp32 MFMA 32x32x2.
 // A[i=row][k] from LDS; contraction split across the lane halves: half h handles k in
@@ -122,10 +140,7 @@ __device__ __forceinline__ void zero_pads(const Ctx& c, int slot, int C) {
   const int np = cp - C;
   if (np <= 0) return;
   const int off = slot_w(c, slot, S_OFF), st = slot_w(c, slot, S_STRIDE);
-  for (int it = threadIdx.x; it < c.T * np; it += NT) {
-    const int r = it / np, j = it - r * np;
-    c.lds[off + r * st + C + j] = 0.f;
-  }
+  for_rc<NT>(c.T, np, [&](int r, int j) { c.lds[off + r * st + C + j] = 0.f; });
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -155,14 +170,15 @@ __device__ __forceinline__ void op_tdense(const Ctx& c, const int* o) {
     scratch[it] = acc;
   }
   __syncthreads();
-  for (int rn = threadIdx.x; rn < TN; rn += NT) {
-    const int r = rn / N, n = rn - r * N;
+  const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0, z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+  for_rc<NT>(c.T, N, [&](int r, int n) {
+    const int rn = r * N + n;
     float z = 0.f;
     for (int s = 0; s < S; ++s) z += scratch[s * TN + rn];
     if (boff >= 0) z += c.params[boff + n];
     c.lds[o_off + r * o_st + n] = epi_fwd(c, e, z, r, n);
-    if (e.zslot >= 0) c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + n] = z;
-  }
+    if (e.zslot >= 0) c.lds[z_off + r * z_st + n] = z;
+  });
   zero_pads<NW>(c, so, N);
 }
 
@@ -182,16 +198,16 @@ __device__ __forceinline__ void op_ew(const Ctx& c, const int* o) {
   const float f0 = __int_as_float(o[O_F0]), f1 = __int_as_float(o[O_F1]);
   const int soff = o[O_AUX0], toff = o[O_AUX1];
   const Epi e = load_epi(o);
-  for (int it = threadIdx.x; it < c.T * C; it += NT) {
-    const int r = it / C, ch = it - r * C;
+  const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0, z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+  for_rc<NT>(c.T, C, [&](int r, int ch) {
     const float va = c.lds[a_off + r * a_st + ch];
     float v;
     if (flags & EW_MUL) v = va * c.lds[b_off + r * b_st + ch];
     else v = (flags & EW_HAS_B) ? f0 * va + f1 * c.lds[b_off + r * b_st + ch] : f0 * va;
     if (flags & EW_AFFINE) v = v * c.params[soff + ch] + (toff >= 0 ? c.params[toff + ch] : 0.f);
     c.lds[o_off + r * o_st + ch] = epi_fwd(c, e, v, r, ch);
-    if (e.zslot >= 0) c.lds[slot_w(c, e.zslot, S_OFF) + r * slot_w(c, e.zslot, S_STRIDE) + ch] = v;
-  }
+    if (e.zslot >= 0) c.lds[z_off + r * z_st + ch] = v;
+  });
   zero_pads<NW>(c, o[O_OUT], C);
 }
 
@@ -527,6 +543,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
 
   const int in_off = slot_w(c, in_slot, S_OFF), in_st = slot_w(c, in_slot, S_STRIDE);
   const int64_t ntiles = (args.nrows + T - 1) / T;
+  const bool small = args.nrows < ((int64_t)1 << 31);
   const int* blk = prog + prog[H_BLK_OFF] + (args.pass * NW + wave) * MAXACC;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -535,17 +552,19 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     // ---- stage the tile's input rows (coalesced 16-B loads, rows contiguous in HBM) ----
     if ((Cin & 3) == 0) {
       const int q = Cin >> 2, qp = slot_w(c, in_slot, S_CP) >> 2;  // pad columns written as 0
-      for (int it = threadIdx.x; it < T * qp; it += NT) {
-        const int r = it / qp, j = it - r * qp;
+      for_rc<NT>(T, qp, [&](int r, int j) {
         const int64_t R = c.row0 + r;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (R < args.nrows && j < q) {
-          const int64_t img = R / args.P, pos = R - img * args.P;
-          const int64_t src = (args.idx ? (int64_t)args.idx[img] : img) * args.P + pos;
+          int64_t src = R;
+          if (args.idx || args.P > 1) {  // 32-bit division when the batch has < 2^31 rows
+            const int64_t img = small ? (int64_t)((int)R / args.P) : R / args.P, pos = R - img * args.P;
+            src = (args.idx ? (int64_t)args.idx[img] : img) * args.P + pos;
+          }
           v = *(const f32x4*)(args.x + src * Cin + 4 * j);
         }
         *(f32x4*)(lds + in_off + r * in_st + 4 * j) = v;
-      }
+      });
     } else {
       const int cp = slot_w(c, in_slot, S_CP);
       for (int it = threadIdx.x; it < T * cp; it += NT) {
@@ -639,11 +658,10 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     }
     if (mode == MODE_FWD) {
       const int o_off = slot_w(c, out_slot, S_OFF), o_st = slot_w(c, out_slot, S_STRIDE);
-      for (int it = threadIdx.x; it < T * Cout; it += NT) {
-        const int r = it / Cout, n = it - r * Cout;
+      for_rc<NT>(T, Cout, [&](int r, int n) {
         const int64_t R = c.row0 + r;
         if (R < args.nrows) args.y[R * Cout + n] = lds[o_off + r * o_st + n];
-      }
+      });
     }
   }
 
