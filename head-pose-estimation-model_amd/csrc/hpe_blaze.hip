@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(512) bf_block_kernel(BfArgs a) {
 
 // CINP / COUTP > 0: channel counts fixed at compile time (every LDS offset of the depthwise taps,
 // W^T rows and the epilogue becomes an immediate; the VALU work per step is then the depthwise FMAs
-// and little else).  0: read from the op words.  Wo >= 32, so a 32-position chunk is one row.
+// and little else).  0: read from the op words.  Wo >= 16 (a power of two): a 32-position chunk is one output row, or two at Wo = 16.
 template <int S, int NC_, int CINP, int COUTP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) bf_rows_kernel(BfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -414,13 +414,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
   auto compute = [&](int oy0) {
     for (int task = wave; task < ntask; task += nwaves) {
       const int chunk = task / ngrp, grp = task - chunk * ngrp;
-      const int oyc = oy0 + ((chunk * 32) >> lgWo);          // the chunk's output row
-      const int x0 = (chunk * 32) & (Wo - 1);
-      int s0 = oyc * S - padt;
+      // a 32-position chunk covers one output row (Wo >= 32) or two (Wo = 16): row oyA, and oyA + 1
+      // for positions past the row end; the lane's depthwise position is p0 + l32
+      const int p0 = chunk * 32;
+      const int oyA = oy0 + (p0 >> lgWo);
+      const int pl = p0 + l32;
+      const int oyl = oy0 + (pl >> lgWo), xl = pl & (Wo - 1);
+      int s0 = oyl * S - padt;
       s0 = (s0 + RING) % RING;
       const int s1 = s0 + 1 == RING ? 0 : s0 + 1;
       const int s2 = s1 + 1 == RING ? 0 : s1 + 1;
-      const int colx = (x0 + l32) * S * CS;
+      const int colx = xl * S * CS;
       const float* r0 = ring + s0 * rowLDS + colx;
       const float* r1 = ring + s1 * rowLDS + colx;
       const float* r2 = ring + s2 * rowLDS + colx;
@@ -446,17 +450,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
           acc[nc] = mfma_split(av, ld4(wb + nc * 32 * KS + c0), acc[nc]);
         }
       }
-      // epilogue: register g <-> position x0 + 4*half + (g&3) + 8*(g>>2) of row oyc
-      const int xh = x0 + 4 * half;
-      const float* rres;
-      const float* rres1 = nullptr;
+      // epilogue: register g <-> step position q = p0 + 4*half + (g&3) + 8*(g>>2): output row
+      // oy0 + (q >> lgWo) (oyA, or oyA + 1 when the chunk wraps), column q & (Wo - 1); the output
+      // address is linear in q.  Residual rows of oyA / oyA + 1 in the ring:
+      const float *rA, *rA1 = nullptr, *rB, *rB1 = nullptr;
       if (S == 1) {
-        rres = ring + (oyc % RING) * rowLDS + (xh + padl) * CS;
+        rA = ring + (oyA % RING) * rowLDS + padl * CS;
+        rB = ring + ((oyA + 1) % RING) * rowLDS + padl * CS;
       } else {
-        rres = ring + ((2 * oyc) % RING) * rowLDS + 2 * xh * CS;
-        rres1 = ring + ((2 * oyc + 1) % RING) * rowLDS + 2 * xh * CS;
+        rA = ring + ((2 * oyA) % RING) * rowLDS;
+        rA1 = ring + ((2 * oyA + 1) % RING) * rowLDS;
+        rB = ring + ((2 * oyA + 2) % RING) * rowLDS;
+        rB1 = ring + ((2 * oyA + 3) % RING) * rowLDS;
       }
-      float* out = a.dst + ((img * Ho + oyc) * Wo + xh) * ostride;
+      float* out = a.dst + ((img * Ho + oy0) * Wo + p0 + 4 * half) * ostride;
 #pragma unroll
       for (int nc = 0; nc < NC; ++nc) {
         const int n = (grp * NC + nc) * 32 + l32;
@@ -468,11 +475,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) b
           const int d = (g & 3) + 8 * (g >> 2);
           float v = acc[nc][g] + bias;
           if (has_res) {
+            const int q = p0 + 4 * half + d;
+            const bool second = (q >> lgWo) != (p0 >> lgWo);
+            const int xg = q & (Wo - 1);
             if (S == 1) {
-              v += rres[d * CS + n];
+              v += (second ? rB : rA)[xg * CS + n];
             } else {
-              const float* t0 = rres + 2 * d * CS + n;
-              const float* t1 = rres1 + 2 * d * CS + n;
+              const float* t0 = (second ? rB : rA) + 2 * xg * CS + n;
+              const float* t1 = (second ? rB1 : rA1) + 2 * xg * CS + n;
               v += fmaxf(fmaxf(t0[0], t0[CS]), fmaxf(t1[0], t1[CS]));
             }
           }
@@ -756,7 +766,7 @@ static int check_op(const int* f, int i) {
     if (f[BFO_WAVES] < 1 || f[BFO_WAVES] > 4) return hpe_fail(HPE_EINVAL, "blazeface op %d: waves", i);
     if (R <= 0 || nseg <= 0 || f[BFO_HO] % nseg || (f[BFO_HO] / nseg) % R) return hpe_fail(HPE_EINVAL, "blazeface op %d: row steps", i);
     const int wo = f[BFO_WO];
-    if (wo < 32 || (wo & (wo - 1)) || (R * wo) % 32) return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel needs Wo >= 32, a power of two", i);
+    if (wo < 16 || (wo & (wo - 1)) || (R * wo) % 32) return hpe_fail(HPE_EINVAL, "blazeface op %d: rows kernel needs Wo >= 16, a power of two", i);
     if (f[BFO_ROWS] != (R - 1) * S + 3 || f[BFO_COLS] != (wo - 1) * S + 3) return hpe_fail(HPE_EINVAL, "blazeface op %d: ring geometry", i);
     if (S == 1 ? (f[BFO_PADT] != 1 || f[BFO_PADL] != 1 || f[BFO_RES] != BF_RES_ID || f[BFO_H] != f[BFO_HO] || f[BFO_W] != wo)
                : (f[BFO_PADT] || f[BFO_PADL] || f[BFO_RES] != BF_RES_MAXPOOL || f[BFO_H] != 2 * f[BFO_HO] || f[BFO_W] != 2 * wo))

@@ -30,6 +30,7 @@ BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT = 1, 2, 3, 4
 import os as _os
 USE_DIRECT = _os.environ.get('HPE_BF_DIRECT', '1') != '0'
 DIRECT_MAX_WO = int(_os.environ.get('HPE_BF_DIRECT_MAX_WO', '8'))
+ROWS_MIN_WO = int(_os.environ.get('HPE_BF_ROWS_MIN_WO', '32'))   # row-streaming kernel from this width
 
 
 def _direct(f, dw, cinp, nct, ks):
@@ -337,7 +338,7 @@ def build_plan(model_config, weights):
         nct = -(-coutp // 32)
         s = bl['stride']
         cs = ks = cinp + 4                                    # (cs/4) odd: conflict-free b128 rows
-        rows_plan = _rows_plan(bl, cinp, nct, ks, cs) if bl['Wo'] >= 32 else None
+        rows_plan = _rows_plan(bl, cinp, nct, ks, cs) if bl['Wo'] >= ROWS_MIN_WO else None
         if rows_plan:
             th, ni, rows, cols, lds, nc, waves = rows_plan
         else:
