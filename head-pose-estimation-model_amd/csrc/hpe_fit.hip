@@ -118,12 +118,13 @@ __device__ __forceinline__ uint64_t get_granule(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// block sum of 5 values (fixed order), scratch: 32 floats; LDS-only barriers (the step's
-// write-through partial stores need not drain here)
+// block sum of 5 values (fixed order), scratch: 32 floats; one LDS-only barrier (the step's
+// write-through partial stores need not drain here).  Called once per step: the previous step's
+// readers of scratch are three barriers back (pass 2 / reduce / optimizer), so no barrier is
+// needed before the writes
 __device__ __forceinline__ void bsum5(float (&v)[5], float* scratch) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) v[k] = wave_sum_dpp(v[k]);
-  bar_lds();
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
     for (int k = 0; k < 5; ++k) scratch[(threadIdx.x >> 6) * 8 + k] = v[k];
