@@ -92,3 +92,31 @@ def test_slot_geometry_conflict_free():
         assert cp % 8 == 0 and cp >= c and st % 4 == 0 and (st // 4) % 2 == 1
         banks = {((st * r) % 64) // 4 for r in range(16)}
         assert len(banks) == 16          # 16 rows x ds_read_b128: distinct bank quads
+
+
+def test_large_programs_multi_pass_and_device_slots():
+    """Round-2 geometry for graphs beyond one launch (csrc/hpe_rowprog.hip H_NPASS / H_GSLOTS): every
+    dW block is owned by exactly one (pass, wave, accumulator) slot, passes are only used when one
+    launch's 16 x 8 accumulators cannot hold the blocks, and slot plans beyond 160 KiB of LDS move to
+    device scratch on the 16-wave kernel."""
+    seen = {}
+    for rid in ('66kjr5zw', '8equl7wt', 's25l3n04', '6togj6se', 'sqnu665j', 'hrchr82r'):
+        mc, w = fixture(rid)
+        p = C.compile_graph(mc, w, 'train', fused=False)
+        wd = p.words
+        npass, gs = int(wd[C.H_NPASS]), int(wd[C.H_GSLOTS])
+        nw, acc = int(wd[C.H_NW]), int(wd[C.H_MAXACC])
+        ndw = p.info['dw_blocks']
+        blk = wd[int(wd[C.H_BLK_OFF]): int(wd[C.H_BLK_OFF]) + npass * nw * acc]
+        used = [int(b) for b in blk if b >= 0]
+        assert len(used) == ndw and len(set(used)) == ndw, rid
+        assert npass == max(1, -(-ndw // (nw * acc))), rid
+        if npass > 1:
+            assert nw == 16 and acc == 8 and ndw > 128, rid
+        if gs:
+            assert nw == C.GS_NW, rid
+        else:
+            assert (int(wd[C.H_LDS_FLOATS]) + 32) * 4 <= 160 * 1024, rid
+        seen[rid] = (npass, gs)
+    assert seen['66kjr5zw'] == (3, 1) and seen['8equl7wt'] == (2, 0) and seen['6togj6se'] == (1, 1)
+    assert seen['sqnu665j'][0] == 1 and seen['hrchr82r'] == (1, 0)
