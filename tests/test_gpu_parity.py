@@ -66,6 +66,15 @@ TRAIN_CASES = [
     ('6togj6se', 'adamax', 77, 2),    # 11-layer residual tanh stack: slots in device scratch
     ('s25l3n04', 'adam', 128, 2),     # 512-256-256-... residual: 3 passes + device-scratch slots
     ('rtomubjl', 'adam', 64, 2),      # 128-wide residual stack with Activation layers and dropout
+    ('rd93oeou', 'adam', 100, 2),     # 256-128-... residual tanh stack: device-scratch slots
+    ('rkq8scme', 'sgd', 90, 2),       # residual stack ending 32-8-3
+    ('rdsncwuy', 'adamax', 128, 2),   # 128-256-512-3 with dropout: 2 passes
+    ('jgbwpv9i', 'adam', 100, 2),     # 512-256-128 residual (no dropout): 3 passes + device slots
+    # create_model(350), dropout 0.01, the fused 12-wave kernel.  SGD: under Adam, weights whose
+    # gradient is near zero (data term cancelling the L2 term) take a +-lr step whose sign is set by
+    # rounding (m / sqrt(v) ~ sign(g)), so no fp32 run tracks the float64 oracle there
+    ('i1tlps36', 'sgd', 128, 2),
+    ('08xjpkmi', 'sgd', 64, 2),       # create_model(360) variant
 ]
 
 
