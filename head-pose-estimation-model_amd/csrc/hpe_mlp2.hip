@@ -35,6 +35,9 @@
 namespace MLP2_NS {
 
 #define MLP2_MAXW 12          // waves per workgroup (hidden width <= 384)
+#ifndef MLP2_W88
+#define MLP2_W88 2
+#endif
 #define MLP2_XS 100             // LDS row stride of an X tile (floats): conflict-free, 16-B aligned
 #define MLP2_XF (32 * MLP2_XS)  // floats per X tile buffer
 #define MLP2_LAB 128            // floats per label buffer: [32 rows][4] (yaw, pitch, roll, pad)
@@ -194,7 +197,7 @@ __device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xf, _Fl
 //   sets the guard word; the exact instantiation launched behind this one then recomputes the
 //   step into the same slabs (and exits at once otherwise).
 template <int KH, int ACT1, bool DROP, int NWM, bool SPLIT>
-__global__ void __launch_bounds__(NWM * 64) mlp2_kernel(Args args) {
+__global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(NWM == MLP2_MAXW || ACT1 < 0 ? 1 : MLP2_W88, 8))) mlp2_kernel(Args args) {
   if (!SPLIT && args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NKB = (2 * KH + 31) / 32;  // 32-row blocks of dW1 (input channels)
