@@ -880,11 +880,25 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
     a.dst2 = f[BFO_SPLIT] ? bufs[f[BFO_DST2]] : nullptr;
     a.nimg = n_images;
     const int64_t tpi = f[BFO_TH] > 0 ? f[BFO_HO] / f[BFO_TH] : 1;
+    const int threads = 64 * f[BFO_WAVES];
+    bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel
+              : f[BFO_KIND] == BF_ROWS ? pick_rows_op(f)
+              : f[BFO_KIND] == BF_DIRECT ? pick_direct(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC])
+                                       : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
     int64_t nwg;
     if (f[BFO_KIND] == BF_DIRECT) {  // persistent: as many workgroups as fit, capped by the tasks
       const int64_t tasks = n_images * ((f[BFO_HO] * f[BFO_WO]) >> 5);
       int per_cu = (160 * 1024) / f[BFO_LDS];
       if (per_cu > 12 / f[BFO_WAVES]) per_cu = 12 / f[BFO_WAVES];
+#ifndef BF_NO_OCC
+      // resident workgroups as the runtime counts them (VGPRs + AGPRs, LDS): a grid sized past
+      // them runs its tasks in a second, partial round
+      int res = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, (const void*)k, threads, f[BFO_LDS]) == hipSuccess &&
+          res > 0 && per_cu > res)
+        per_cu = res;
+#endif
       if (per_cu < 1) per_cu = 1;
       nwg = (tasks + f[BFO_WAVES] - 1) / f[BFO_WAVES];
       if (nwg > (int64_t)h->n_cu * per_cu) nwg = (int64_t)h->n_cu * per_cu;
@@ -894,12 +908,6 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
     }
     if (nwg > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
     a.nwg = (int)nwg;
-    const int threads = 64 * f[BFO_WAVES];
-    bf_fn k = f[BFO_KIND] == BF_STEM ? bf_stem_kernel
-              : f[BFO_KIND] == BF_ROWS ? pick_rows_op(f)
-              : f[BFO_KIND] == BF_DIRECT ? pick_direct(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC])
-                                       : pick_block(f[BFO_STRIDE], f[BFO_DW], f[BFO_NC]);
-    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(threads), f[BFO_LDS], s, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hpe_fail(HPE_ERUNTIME, "blazeface op %d launch: %s", i, hipGetErrorString(e));

@@ -913,6 +913,14 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   } else {
     kfn_t k = pick_kernel(nw, words[H_MAXACC], gs);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes_of(words));
+#ifndef RP_NO_OCC
+    // the persistent grid no larger than the workgroups that are resident at once as the runtime
+    // counts them (VGPRs + AGPRs of the instantiation, LDS): past that the tiles run in a second round
+    int res = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, (const void*)k, nw * 64, lds_bytes_of(words)) == hipSuccess &&
+        res > 0 && res < per_cu)
+      p->grid_cap = ncu * res;
+#endif
     if (gs) {
       e = hipMalloc(&p->gscr, (size_t)p->grid_cap * words[H_LDS_FLOATS] * sizeof(float));
       if (e != hipSuccess) {
