@@ -90,10 +90,40 @@ def launch_plan(gpus, argv, env):
             os.path.abspath(__file__)] + list(argv)
 
 
+KFD_NODES = '/sys/class/kfd/kfd/topology/nodes'
+
+
+def visible_gpus(env=None, kfd=KFD_NODES):
+    """GPUs this job may use, counted WITHOUT the HIP runtime (the launcher must not initialise a
+    device before its ranks start): the visible-devices list when one is set
+    (ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, the most restrictive wins),
+    else the KFD topology nodes that are GPUs (simd_count > 0).  0 when neither is available."""
+    env = os.environ if env is None else env
+    lists = [env[k] for k in ('ROCR_VISIBLE_DEVICES', 'HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES')
+             if env.get(k) is not None]
+    n_kfd = 0
+    try:
+        for node in os.listdir(kfd):
+            try:
+                with open(os.path.join(kfd, node, 'properties')) as fh:
+                    props = dict(l.split()[:2] for l in fh if len(l.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get('simd_count', '0')) > 0:
+                n_kfd += 1
+    except OSError:
+        pass
+    counts = [len([d for d in l.split(',') if d.strip() != '']) for l in lists]
+    if counts:
+        return min(counts + ([n_kfd] if n_kfd else []))
+    return n_kfd
+
+
 def spawn_ranks(gpus, argv):
-    """Run ``gpus`` ranks as a child torchrun job; returns its exit code.  Counting devices with
-    torch.cuda.device_count() does not initialise the GPU on this image."""
-    n_dev = torch.cuda.device_count()
+    """Run ``gpus`` ranks as a child torchrun job; returns its exit code.  The GPUs are counted
+    from the visible-devices env / KFD sysfs (visible_gpus), never through HIP: this process only
+    launches the ranks."""
+    n_dev = visible_gpus()
     if n_dev < gpus:
         print('bench.py: --gpus %d requested but only %d GPU(s) visible' % (gpus, n_dev), file=sys.stderr)
         return 2

@@ -22,6 +22,7 @@
 // non-finite split accumulator sets a flag and the host re-runs the epoch on the exact path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/hpe.h"
 #include "hpe_common.h"
@@ -31,7 +32,9 @@
 #define FIT_XS 100             // LDS row stride of an X tile (floats)
 #define FIT_XT (32 * FIT_XS)   // floats per X tile
 #define FIT_SLOTS 2            // resident X tiles per wave (batch <= 256 stays in LDS across the exchange)
-#define FIT_MAX_BATCH 256      // batch rows (<= 2 tiles per wave: X stays in LDS across the exchange)
+#define FIT_RES_BATCH 256      // batch rows whose X tiles stay resident across the exchange
+#define FIT_MAX_BATCH 512      // batch rows: beyond FIT_RES_BATCH the tiles are re-gathered for the
+                               // backward and the partial table overlays the X slots
 #define FIT_UNION 9216         // floats: A1 park | head-partial table [G][batch][3] | dW1 reduce
 #define FIT_POLL 24            // granules in flight per thread in the exchange
 #define FIT_PART_OFF 128       // workspace (words): [1] flags, [2..3] debug, [4..4+G) XCC ids, [128..] granules
@@ -58,6 +61,7 @@ struct FitArgs {
   float* stats;             // [steps][stats_stride]: sse, sae, reg_0 .. reg_{G-1}
   int stats_stride;
   int* sync;                // workspace
+  int spin_limit;           // exchange polls before the timeout flag (< 0: flag at once, tests only)
   int64_t n_params, n_mirror, n_train, n_ws_granules;  // sizes (FIT_DEBUG bounds checks)
   uint64_t* part;           // workspace + FIT_PART_OFF: [2][G][3][bs] granules {float bits, tag}
 };
@@ -199,7 +203,10 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
   float* misc = lds + FIT_L_MISC;
   float* a1p = lds + FIT_L_UNION + wave * 1024;  // pass 1: this wave's A1 park [16][64]
   float* dwr = lds + FIT_L_UNION;                // after pass 2: dW1 reduce [2][3][16][64]
-  float* ptab = lds + FIT_L_UNION;               // exchange: every workgroup's partials [G][bs][3]
+  // exchange: every workgroup's partials [G][3][bs]; batches beyond FIT_RES_BATCH re-gather X for
+  // the backward, so their (larger) table overlays the X slots
+  const bool bigbatch = a.bs > FIT_RES_BATCH;
+  float* ptab = lds + (bigbatch ? FIT_L_XS : FIT_L_UNION);
 
   // ---- owned parameters (fp32 master in LDS / registers, optimizer state in registers, for the
   //      whole epoch) ----
@@ -290,7 +297,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     const float inv_count = 1.f / (float)(nb * 3);
     const uint64_t seed = a.seed_base + (uint64_t)(a.iter0 + 1 + s);
     const int tw = (ntile - wave + FIT_NW - 1) / FIT_NW;  // tiles of this wave: wave, wave + 4, ...
-    const bool resident = ntile <= FIT_NW * FIT_SLOTS;
+    const bool resident = !bigbatch && ntile <= FIT_NW * FIT_SLOTS;
 
     // ---- this step's weight fragments (from the post-update tables) ----
     SplitW wsp[SPLIT ? 6 : 1];
@@ -429,13 +436,18 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     // workgroup gets the same p
     const bool pair = ntile * 32 * 2 <= FIT_NW * 64;
     const int rr = pair ? ((tid >> 6) << 5) + (tid & 31) : tid;
-    float ylab[3] = {0.f, 0.f, 0.f};
-    if (rr < nb) {
-      const int src = FIT_OK(bperm - a.perm + rr, a.n, 8) ? bperm[rr] : 0;
-      if (FIT_OK(src, a.n, 9)) {
-        ylab[0] = a.ytrue[(int64_t)src * 3 + 0];
-        ylab[1] = a.ytrue[(int64_t)src * 3 + 1];
-        ylab[2] = a.ytrue[(int64_t)src * 3 + 2];
+    // (batch > 256: rows rr and rr + 256)
+    float ylab[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ry = rr + h * FIT_NW * 64;
+      if (ry < nb) {
+        const int src = FIT_OK(bperm - a.perm + ry, a.n, 8) ? bperm[ry] : 0;
+        if (FIT_OK(src, a.n, 9)) {
+          ylab[h][0] = a.ytrue[(int64_t)src * 3 + 0];
+          ylab[h][1] = a.ytrue[(int64_t)src * 3 + 1];
+          ylab[h][2] = a.ytrue[(int64_t)src * 3 + 2];
+        }
       }
     }
     bar_lds();  // every wave's pass 1 done with its A1 park (ptab overlays it)
@@ -472,7 +484,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
 #ifdef FIT_STAMPS
             if (tid == 0) ph[7] += 1;
 #endif
-            if (++it > (1 << 22)) { flags |= FIT_FLAG_TIMEOUT; break; }
+            if (++it > a.spin_limit) { flags |= FIT_FLAG_TIMEOUT; break; }
             __builtin_amdgcn_s_sleep(1);
 #pragma unroll
             for (int u = 0; u < FIT_POLL; ++u)
@@ -481,13 +493,14 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
         }
       }
     }
+    if (a.spin_limit < 0) flags |= FIT_FLAG_TIMEOUT;
     if (flags & FIT_FLAG_TIMEOUT) misc[40] = 1.f;
     FSTAMP(8);
     bar_lds();
     FSTAMP(9);
     if (misc[40] != 0.f) { flags |= FIT_FLAG_TIMEOUT; break; }
     const int cpar = pair ? half : 0, cstep = pair ? 2 : 1;
-    for (int r = rr; r < ntile * 32 && (!pair || r < 128); r += blockDim.x) {
+    for (int r = rr, h = 0; r < ntile * 32 && (!pair || r < 128); r += blockDim.x, ++h) {
       f32x4 d = {0.f, 0.f, 0.f, 0.f};
       {
         float p[3] = {0.f, 0.f, 0.f};
@@ -515,7 +528,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
             k2 = drop_hash(seed, drop2, (uint64_t)r, j) >= thr2;
             pj = k2 ? pj / keep2 : 0.f;
           }
-          const float err = pj - ylab[j];
+          const float err = pj - ylab[h][j];
           red5[0] = fmaf(err, err, red5[0]);
           red5[1] += fabsf(err);
           float gj = 2.f * err;
@@ -754,7 +767,20 @@ extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
   if (o[O_N] < 1 || (o[O_N] + 31) / 32 > 32) return 0;  // 8 G <= 256 workgroups
   if (!fit_pick(w, true)) return 0;
   const int G = (o[O_N] + 31) / 32;
-  return batch >= 1 && batch <= FIT_MAX_BATCH && G * batch * 3 <= FIT_UNION;
+  if (batch < 1 || batch > FIT_MAX_BATCH) return 0;
+  // partial table: the LDS union (resident X) or the X slots (batch > FIT_RES_BATCH)
+  if (G * batch * 3 > (batch > FIT_RES_BATCH ? FIT_NW * FIT_SLOTS * FIT_XT : FIT_UNION)) return 0;
+  // the G working workgroups spin on each other's partials, so all must be resident at once: one
+  // per CU (LDS), on the XCD the blockIdx % 8 == 0 workgroups are dispatched to
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  fit_fn k = fit_pick(w, true);
+  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, FIT_LDS_BYTES) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k, FIT_NW * 64, FIT_LDS_BYTES) != hipSuccess)
+    return 0;
+  return occ >= 1 && G <= cus / 8;
 }
 
 extern "C" size_t hpe_fit_workspace_size(const hpe_program* p, int32_t batch) {
@@ -793,6 +819,10 @@ extern "C" int hpe_fit_epoch(const hpe_program* p, float* params, float* params_
   a.n_ws_granules = (int64_t)2 * G * batch * 3;
   a.sync = (int*)workspace;
   a.part = (uint64_t*)((float*)workspace + FIT_PART_OFF);
+  {
+    const char* e = getenv("HPE_FIT_FORCE_TIMEOUT");  // tests: the host's timeout rollback
+    a.spin_limit = (e && e[0] == '1') ? -1 : (1 << 22);
+  }
   hipStream_t s = (hipStream_t)stream;
   // flags and granules: no tag of an earlier launch (an exact re-run, or iterations restored from
   // a checkpoint) can match this launch's

@@ -6,6 +6,7 @@ arithmetic op of the hot path runs in libhpe.so (csrc/hpe_rowprog.hip) through t
 """
 import ctypes
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -196,6 +197,8 @@ class Engine:
         maps, the 2-layer create_model family, one rank); HPE_FIT_FUSED=0 forces the per-step path."""
         if world != 1 or P != 1 or os.environ.get('HPE_FIT_FUSED', '1') == '0':
             return False
+        if getattr(self, '_fit_disabled', False):   # an earlier epoch launch timed out
+            return False
         c = self.program('train', 1)
         return c.prog.kind == 'mlp2' and _lib.load().hpe_fit_supported(c.h, int(batch)) == 1
 
@@ -218,10 +221,17 @@ class Engine:
             a = np.full(steps, lr)
         return torch.from_numpy(a.astype(np.float32)).to(self.device)
 
+    def _restore(self, saved):
+        for dst, src in zip([t for t in (self.params, self.params_t, self.m, self.v) if t is not None], saved):
+            dst.copy_(src)
+
     def fit_epoch(self, opt, x, y, perm, batch, stats, seed_base):
         """One epoch of fit: ceil(n / batch) steps over rows perm (device int32) of x / y in one
         launch; stats: device [steps, >= 2 + G].  A flagged fp16-split overflow re-runs the epoch
-        on the exact-fp32 path from the saved state."""
+        on the exact-fp32 path from the saved state.  A workgroup-exchange timeout (flag 2: the G
+        workgroups were not all resident, e.g. another job held CUs) leaves workgroups at different
+        steps, so the saved parameters / Adam state are restored, the fused path is disabled for this
+        engine, and None is returned: the caller re-runs the epoch on the per-step path."""
         c = self.program('train', 1)
         lib = _lib.load()
         kind = OPT_KIND[opt.kind]
@@ -247,10 +257,12 @@ class Engine:
 
         flags = launch(0)
         if flags & 1:  # fp16 range exceeded somewhere: redo the epoch exactly
-            for dst, src in zip([t for t in (self.params, self.params_t, self.m, self.v) if t is not None], saved):
-                dst.copy_(src)
+            self._restore(saved)
             flags = launch(1)
         if flags & 2:
-            raise _lib.HPEError('hpe_fit_epoch: workgroup exchange timed out')
+            self._restore(saved)
+            self._fit_disabled = True
+            warnings.warn('hpe_fit_epoch: workgroup exchange timed out; epoch re-run on the per-step path')
+            return None
         self.iterations += steps
         return steps

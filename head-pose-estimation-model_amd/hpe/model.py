@@ -271,7 +271,10 @@ class Model:
             nbs = [min(n, (s + 1) * bs) - s * bs for s in range(steps)]
             if fused:
                 stats.zero_()
-                eng.fit_epoch(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0))
+                if eng.fit_epoch(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0)) is None:
+                    # the epoch launch timed out and was rolled back: this and later epochs per step
+                    fused = self._last_fit_fused = False
+                    stats = torch.zeros((steps, 2 + og), dtype=torch.float32, device=eng.device)
             for s in range(0 if fused else steps):
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0

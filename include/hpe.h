@@ -108,8 +108,12 @@ int hpe_optim_grid(int64_t n);
  * loss on the pre-update weights is the sum of the reg_g).  exact != 0 runs exact-fp32 MFMA GEMMs.
  * workspace: hpe_fit_workspace_size bytes; after the launch its int word [1] holds flags
  * (1: a split accumulator was non-finite — rerun the epoch with exact = 1 from the saved state;
- * 2: the per-step workgroup exchange timed out).  hpe_fit_supported: 1 if program + batch qualify
- * (batch <= 512). */
+ * 2: the per-step workgroup exchange timed out — the workgroups may have stopped at different
+ * steps, so restore params / m / v and run the epoch per step).  hpe_fit_supported: 1 if program
+ * + batch qualify: F <= 1024 (G <= 32), batch <= 512, the exchange table G * batch * 3 floats
+ * within 9,216 (batch <= 256) or 25,600 (batch 257..512), and all G workgroups co-resident (one
+ * per CU, G <= CUs / 8); 0 otherwise (and without a device).  Env HPE_FIT_FORCE_TIMEOUT=1 (tests)
+ * raises flag 2 at the first exchange. */
 int hpe_fit_supported(const hpe_program *prog, int32_t batch);
 size_t hpe_fit_workspace_size(const hpe_program *prog, int32_t batch);
 int hpe_fit_epoch(const hpe_program *prog, float *params, float *params_t, float *m, float *v,

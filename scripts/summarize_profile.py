@@ -10,8 +10,16 @@ Inputs (gpurun_out/, merged back by gpurun):
   prof_<tag>_<line>/**/*kernel_stats.csv        rocprofv3 --kernel-trace --stats
   prof_<tag>_<line>/**/*kernel_trace.csv        per-dispatch trace (durations keyed by grid)
   pmc_<tag>_<line>_<pass>/**/*counter_collection.csv   rocprofv3 --pmc, one pass per counter group
+Timed region only: rocprofv3's own --stats summary averages every dispatch of a
+process, including the bench's untimed warm-up launches (the first one cold), so its average can
+exceed the bench's step time.  The per-line averages here keep only the LAST ``timed`` iterations'
+dispatches of each (kernel, grid) group, where ``timed`` / ``warm`` are the bench line's own loop
+counts for ``bench.py --only <line> --steps S --warmup W`` (``loop_counts``); a group launched k times
+per iteration keeps its last k * timed dispatches.
+
 Outputs:
-  profiles/<tag>_<line>_kernel_stats.csv        copy of the stats summary
+  profiles/<tag>_<line>_kernel_stats.csv        copy of rocprofv3's stats summary (all dispatches)
+  profiles/<tag>_<line>_kernel_stats_timed.csv  the same columns over the timed-region dispatches
   profiles/<tag>_<line>_pmc.csv                 per (kernel, grid): dispatches, mean of every counter
   profiles/traffic.json                         per line: dominant kernel, avg duration, HBM bytes per
                                                 launch, SQ-derived utilisation; read by bench.py
@@ -71,21 +79,69 @@ def mean(v):
     return sum(v) / len(v) if v else 0.0
 
 
-def summarize_line(tag, line):
+def loop_counts(line, steps, warmup):
+    """(warm-up iterations, timed iterations) of ``bench.py --only <line> --steps steps --warmup
+    warmup`` -- mirrors the loops in bench.py (train: run_train(steps, warmup); train88: 2 warm-ups,
+    max(5, min(steps, 20)) timed; infer: 3 / max(10, steps); blazeface and attn: 3 / max(10, steps)
+    forwards)."""
+    if line == 'train':
+        return warmup, steps
+    if line == 'train88':
+        return 2, max(5, min(steps, 20))
+    if line in ('infer', 'blazeface', 'attn'):
+        return 3, max(10, steps)
+    return 0, None
+
+
+def timed_only(groups, warm, timed):
+    """Keep each group's dispatches of the last ``timed`` iterations (k per iteration when the
+    group's count is a multiple of warm + timed; a group that does not repeat per iteration, e.g.
+    one-off setup launches, is dropped)."""
+    if timed is None:
+        return dict(groups)
+    out = {}
+    it = warm + timed
+    for key, v in groups.items():
+        if len(v) >= it and len(v) % it == 0:
+            k = len(v) // it
+            out[key] = v[-k * timed:]
+    return out
+
+
+def write_stats(path, groups):
+    """rocprofv3 --stats columns, one row per kernel name (grids merged), sorted by total time."""
+    by = defaultdict(list)
+    for (name, _grid), v in groups.items():
+        by[name].extend(v)
+    tot_all = sum(sum(v) for v in by.values()) or 1
+    with open(path, 'w', newline='') as fh:
+        wr = csv.writer(fh, quoting=csv.QUOTE_NONNUMERIC)
+        wr.writerow(['Name', 'Calls', 'TotalDurationNs', 'AverageNs', 'Percentage', 'MinNs', 'MaxNs'])
+        for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+            wr.writerow([name, len(v), sum(v), sum(v) / len(v), 100.0 * sum(v) / tot_all, min(v), max(v)])
+
+
+def summarize_line(tag, line, steps=10, warmup=2, pmc_steps=5, pmc_warmup=1):
     tdir = os.path.join(OUT, 'prof_%s_%s' % (tag, line))
     stats = _one(os.path.join(tdir, '**', '*kernel_stats.csv'))
     trace = _one(os.path.join(tdir, '**', '*kernel_trace.csv'))
     res = {}
     if stats:
         shutil.copy(stats, os.path.join(PROF, '%s_%s_kernel_stats.csv' % (tag, line)))
-    groups = trace_groups(trace) if trace else {}
+    all_groups = trace_groups(trace) if trace else {}
+    warm, timed = loop_counts(line, steps, warmup)
+    groups = timed_only(all_groups, warm, timed)
+    if groups:
+        write_stats(os.path.join(PROF, '%s_%s_kernel_stats_timed.csv' % (tag, line)), groups)
     ctr = defaultdict(dict)
     for p in sorted(glob.glob(os.path.join(OUT, 'pmc_%s_%s_*' % (tag, line)))):
         f = _one(os.path.join(p, '**', '*counter_collection.csv'))
         if not f:
             continue
+        pw, pt = loop_counts(line, pmc_steps, pmc_warmup)
         for key, cs in counter_groups(f).items():
             for c, vals in cs.items():
+                vals = timed_only({key: vals}, pw, pt).get(key) or vals
                 ctr[key][c] = (len(vals), mean(vals))
     if ctr:
         names = sorted({c for v in ctr.values() for c in v})
@@ -99,7 +155,7 @@ def summarize_line(tag, line):
     if not groups:
         return res
     if line == 'blazeface':
-        # one forward = every launch of the graph; forwards = dispatches of the stem
+        # one forward = every launch of the graph; forwards = dispatches of the stem (timed only)
         nfwd = max(1, min(len(v) for k, v in groups.items() if k[0].startswith('bf_stem')))
         tot_ns = sum(sum(v) for v in groups.values()) / nfwd
         fb = wb = 0.0
@@ -109,13 +165,15 @@ def summarize_line(tag, line):
             if 'WRITE_SIZE' in cs:
                 wb += 1024 * cs['WRITE_SIZE'][1] * cs['WRITE_SIZE'][0]
         res = {'kernel': 'all launches of one forward (bf_* + head GEMMs + regressor programs)',
-               'avg_ns': tot_ns, 'forwards': nfwd}
+               'avg_ns': tot_ns, 'forwards': nfwd, 'timed_region_only': True}
         if ctr:
             res.update({'fetch_bytes': fb / nfwd, 'write_bytes': wb / nfwd, 'hbm_bytes_per_launch': (fb + wb) / nfwd})
         return res
     key = max(groups, key=lambda k: sum(groups[k]))
     d = groups[key]
     res = {'kernel': key[0], 'grid': key[1], 'dispatches': len(d), 'avg_ns': mean(d),
+           'min_ns': min(d), 'timed_region_only': timed is not None,
+           'avg_ns_all_dispatches': mean(all_groups[key]),
            'share_of_line_time': sum(d) / sum(sum(v) for v in groups.values())}
     cs = ctr.get(key)
     if cs:
@@ -145,7 +203,7 @@ def summarize_line(tag, line):
     return res
 
 
-def main(tag, lines):
+def main(tag, lines, steps=10, warmup=2):
     os.makedirs(PROF, exist_ok=True)
     path = os.path.join(PROF, 'traffic.json')
     out = {}
@@ -155,20 +213,24 @@ def main(tag, lines):
         if out.get('tag') != tag:      # never mix an older round's numbers into this one
             out = {}
     for line in lines:
-        r = summarize_line(tag, line)
+        r = summarize_line(tag, line, steps, warmup)
         if r:
-            r['source'] = 'profiles/%s_%s_kernel_stats.csv, %s_%s_pmc.csv' % (tag, line, tag, line)
+            r['source'] = ('profiles/%s_%s_kernel_stats_timed.csv (timed-region dispatches of %s_%s_kernel_'
+                           'stats.csv), %s_%s_pmc.csv' % (tag, line, tag, line, tag, line))
             out[line] = r
     out['tag'] = tag
-    out['note'] = ('per bench line, profiled in its own process; FETCH_SIZE x 2 x 1024, WRITE_SIZE x 1024 '
+    out['note'] = ('per bench line, profiled in its own process (bench.py --only <line> --steps %d --warmup %d); '
+                   'avg_ns over the timed-region dispatches only; FETCH_SIZE x 2 x 1024, WRITE_SIZE x 1024 '
                    '(gfx950, MI355X_MICROARCH.md); mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / '
-                   '(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)')
+                   '(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)' % (steps, warmup))
     with open(path, 'w') as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
-    tag = sys.argv[1] if len(sys.argv) > 1 else 'r02'
-    lines = sys.argv[2].split(',') if len(sys.argv) > 2 else ['train', 'infer', 'train88', 'blazeface', 'p1']
-    main(tag, lines)
+    tag = sys.argv[1] if len(sys.argv) > 1 else 'r03'
+    lines = sys.argv[2].split(',') if len(sys.argv) > 2 else ['train', 'infer', 'train88', 'blazeface', 'p1', 'attn']
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    warmup = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    main(tag, lines, steps, warmup)

@@ -32,3 +32,38 @@ def test_gpus_2_without_gpus_fails_cleanly():
     assert r.returncode == 2, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
     assert 'GPU(s) visible' in r.stderr
     assert r.stdout.strip() == ''
+
+
+def _kfd(tmp_path, kinds):
+    for i, simd in enumerate(kinds):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / 'properties').write_text('cpu_cores_count 0\nsimd_count %d\nlds_size_in_kb 160\n' % simd)
+    return str(tmp_path)
+
+
+def test_visible_gpus_counts_without_hip(tmp_path, monkeypatch):
+    """the launcher counts GPUs from KFD sysfs / the visible-devices env; torch's device
+    count (which can initialise HIP in the parent) is never called."""
+    import bench
+
+    def boom(*a, **k):
+        raise AssertionError('launcher touched the HIP runtime')
+    monkeypatch.setattr(torch.cuda, 'device_count', boom)
+    monkeypatch.setattr(torch.cuda, 'is_available', boom)
+    kfd = _kfd(tmp_path, [0, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 1024])  # 1 CPU + 8 GPU nodes
+    assert bench.visible_gpus({}, kfd) == 8
+    assert bench.visible_gpus({'HIP_VISIBLE_DEVICES': '0,1'}, kfd) == 2
+    assert bench.visible_gpus({'ROCR_VISIBLE_DEVICES': '3', 'HIP_VISIBLE_DEVICES': '0,1'}, kfd) == 1
+    assert bench.visible_gpus({'CUDA_VISIBLE_DEVICES': ''}, kfd) == 0
+    assert bench.visible_gpus({}, str(tmp_path / 'absent')) == 0
+    monkeypatch.setattr(bench, 'KFD_NODES', kfd)
+    calls = []
+    monkeypatch.setattr(bench.subprocess, 'call', lambda cmd, env=None: calls.append(cmd) or 0)
+    monkeypatch.delenv('HIP_VISIBLE_DEVICES', raising=False)
+    monkeypatch.delenv('ROCR_VISIBLE_DEVICES', raising=False)
+    monkeypatch.delenv('CUDA_VISIBLE_DEVICES', raising=False)
+    monkeypatch.setattr(bench, 'visible_gpus', lambda env=None, kfd=kfd: 8)
+    assert bench.spawn_ranks(8, ['--gpus', '8']) == 0
+    assert calls and calls[0][2] == 'torch.distributed.run'
+    assert not torch.cuda.is_initialized()

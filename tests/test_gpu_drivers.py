@@ -101,3 +101,49 @@ def test_data_parallel_fit_matches_single_device(tmp_path):
     np.testing.assert_allclose(dp['loss'], h.history['loss'], rtol=1e-5)
     for k, v in m.weights_dict().items():
         np.testing.assert_allclose(dp[k.replace('/', '|')], v, rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+def _bench_worker(rank, world, port, out):
+    for p in (ROOT, PKG, os.path.dirname(os.path.abspath(__file__))):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import bench
+    import hpe as H
+    from hpe import keras as kk
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    H.set_seed(42)
+    kk.backend.clear_session()
+    m = bench.build_train_model(kk)
+    eng = m._eng()
+    dev = torch.device('cuda', 0)
+    P, n_loc = 64, 12
+    x, y = bench.synth(n_loc * world, 7, dev, P=P)   # the global batch; this rank takes its slice
+    xs, ys = x[rank * n_loc * P:(rank + 1) * n_loc * P].contiguous(), y[rank * n_loc:(rank + 1) * n_loc].contiguous()
+    dt, kms, mse = bench.run_train(eng, m.optimizer, xs, ys, P, n_loc, n_loc * world, rank, world, 3, 1, dist)
+    if rank == 0:
+        np.savez(out, mse=mse, dt=dt, **{k.replace('/', '|'): v for k, v in m.weights_dict().items()})
+    dist.destroy_process_group()
+
+
+def test_bench_run_train_two_ranks_matches_one(tmp_path):
+    """bench.run_train itself (the timed loop of the headline / strong lines) on
+    2 gloo ranks sharing one GPU, each taking its slice of the global batch, gives the weights of
+    one rank training on the whole batch (one all-reduce of the flat gradient per step)."""
+    import torch.multiprocessing as mp
+    import bench
+    out = str(tmp_path / 'b.npz')
+    mp.spawn(_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    dp = np.load(out)
+    hpe.set_seed(42)
+    hpe.keras.backend.clear_session()
+    m = bench.build_train_model(hpe.keras)
+    dev = torch.device('cuda', 0)
+    P, n = 64, 24
+    x, y = bench.synth(n, 7, dev, P=P)
+    _, _, mse = bench.run_train(m._eng(), m.optimizer, x, y, P, n, n, 0, 1, 3, 1, None)
+    assert float(dp['mse']) == pytest.approx(mse, rel=1e-4)
+    for k, v in m.weights_dict().items():
+        np.testing.assert_allclose(dp[k.replace('/', '|')], v, rtol=1e-4, atol=1e-6, err_msg=k)

@@ -69,6 +69,10 @@ CASES = [  # (model source, F, act, dropout, optimizer, lr, batch, rows, epochs)
     ('new', 256, 'relu', 0.1, 'adamax', 2.8e-4, 200, 601, 2),           # runtime activation, ragged batch
     ('new', 16, 'tanh', 0.0, 'sgd', 0.05, 128, 300, 3),                 # one workgroup, SGD
     ('new', 100, 'elu', 0.3, 'adam', 1e-3, 32, 97, 2),                  # tiny batches, partial last
+    # batches beyond 256: X re-gathered for the backward, partial table over the X slots
+    ('sqnu665j', 360, 'tanh', 0.0, 'adam', 2.8e-4, 512, 1100, 2),       # p1 b512; last batch 76
+    ('stoqa9pt', 64, 'softsign', 1e-4, 'adam', 2.8e-4, 512, 1300, 2),   # configs[2]: Model-88, Adam, b512
+    ('new', 384, 'tanh', 0.1, 'sgd', 0.01, 300, 901, 2),                # 12 workgroups, batch 300
 ]
 
 
@@ -142,3 +146,30 @@ def test_fused_epoch_reference_data_train_96():
             os.environ.pop('HPE_FIT_FUSED')
     for k in ('loss', 'mae', 'val_loss', 'val_mae'):
         np.testing.assert_allclose(hs[0].history[k], hs[1].history[k], rtol=1e-4, err_msg=k)
+
+
+def test_fused_epoch_timeout_rolls_back_to_per_step():
+    """a workgroup-exchange timeout (forced: HPE_FIT_FORCE_TIMEOUT=1) leaves the
+    workgroups at different steps; the engine restores the saved parameters / Adam state, disables
+    the fused path and runs the epoch per step -- the result is the per-step path's."""
+    m0 = _model('sqnu665j')
+    w0 = m0.weights_dict()
+    x = features(400, 96, seed=21)
+    y = labels(400, seed=22)
+    mf = hpe.model_from_config(m0.model_config, w0)
+    os.environ['HPE_FIT_FORCE_TIMEOUT'] = '1'
+    try:
+        hpe.set_seed(5)
+        mf.compile(optimizer=OPT['adam'](learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+        with pytest.warns(UserWarning, match='timed out'):
+            hf = mf.fit(x, y, batch_size=128, epochs=2, verbose=0)
+    finally:
+        os.environ.pop('HPE_FIT_FORCE_TIMEOUT')
+    assert mf._last_fit_fused is False and mf._eng()._fit_disabled
+    mp = hpe.model_from_config(m0.model_config, w0)
+    hp = _fit(mp, 'adam', 2.8e-4, x, y, 128, 2, fused=False)
+    wf, wp = mf.weights_dict(), mp.weights_dict()
+    for k in wf:
+        np.testing.assert_array_equal(wf[k], wp[k], err_msg=k)
+    np.testing.assert_allclose(hf.history['loss'], hp.history['loss'], rtol=1e-6)
+    assert mf._eng().iterations == mp._eng().iterations == 2 * 4

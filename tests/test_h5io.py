@@ -249,3 +249,30 @@ def test_gpu_checkpoint_resume_is_exact(tmp_path):
     c.fit(x, y, batch_size=64, epochs=2, shuffle=False, verbose=0)
     for wa, wc in zip(a.get_weights(), c.get_weights()):
         np.testing.assert_array_equal(wa, wc)
+
+
+def test_no_reference_bytecode_in_committed_fixtures():
+    """reference Lambda bytecode must not travel in any form.  Every committed .h5 /
+    .json fixture's Lambda 'function' field is the stripped placeholder (raw attribute, before the
+    reader's own stripping), and no file holds a base64 marshalled code object (0xe3 header)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        'strip_h5_bytecode', os.path.join(os.path.dirname(H5), 'strip_h5_bytecode.py'))
+    sb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sb)
+    n_lambda = 0
+    for p in glob.glob(os.path.join(H5, '*.h5')):
+        fns = sb.lambda_functions(sb.raw_model_config(p))
+        n_lambda += len(fns)
+        assert all(f == '<bytecode stripped>' for f in fns), p
+    for p in glob.glob(os.path.join(MODELS, '*.json')):
+        with open(p) as fh:
+            d = json.load(fh)
+        mc = d.get('model_config', d)
+        if isinstance(mc, dict):
+            assert all(f == '<bytecode stripped>' for f in sb.lambda_functions(mc)), p
+    assert n_lambda >= 2                     # ker7z9mv's reshape_flat / reshape_back
+    for p in glob.glob(os.path.join(H5, '*.h5')) + glob.glob(os.path.join(MODELS, '*.json')):
+        with open(p, 'rb') as fh:
+            raw = fh.read()
+        assert b'4wEAAAAA' not in raw and b'4wAAAAAA' not in raw, p
