@@ -169,6 +169,15 @@ __device__ __forceinline__ int fit_src(const FitArgs& a, const int* bperm, int r
   const int lr = min(r0 + (lane & 31), nb - 1);
   return FIT_OK(bperm - a.perm + lr, a.n, 1) ? bperm[lr] : 0;
 }
+// as fit_stage_src with the 32 source rows in lanes lo .. lo + 31 of src (two tiles per VGPR)
+__device__ __forceinline__ void fit_stage_pair(const FitArgs& a, float* xt, int src, int lo, int Cin, int lane) {
+  const int q = Cin >> 2;
+#pragma unroll 4
+  for (int r = 0; r < 32; ++r) {
+    const int64_t s = (int64_t)__builtin_amdgcn_readlane(src, lo + r);
+    if (lane < q && FIT_OK(s, a.n, 2)) glds16(a.x + s * Cin + 4 * lane, lds_addr(xt + r * FIT_XS));
+  }
+}
 __device__ __forceinline__ void fit_stage(const FitArgs& a, float* xt, const int* bperm, int r0, int nb, int Cin,
                                           int lane) {
   const int src = fit_src(a, bperm, r0, nb, lane);
@@ -380,13 +389,32 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     // the next step's tile is prefetched during this step's backward; A1 stays in registers
     const uint32_t tag = (uint32_t)(a.iter0 + 1 + s);
     uint64_t* part_out = a.part + ((size_t)(s & 1) * G + c) * a.bs * 3;  // [3][bs]
+    // several tiles per wave (batch > 128): the source rows of all of them are looked up at once
+    // (two tiles per VGPR: tile i's row r in lane 32 (i & 1) + r of srcp[i >> 1]), and tile i + 1
+    // streams in while tile i computes (32 LDS-DMA pieces per tile: vmcnt(32) = tile i landed)
     f32x16 a1keep = {};
     uint32_t kmkeep = 0;
+    int srcp0 = 0, srcp1 = 0;
+    if (!onetile) {
+      const int r32 = lane & 31, hi = lane >> 5;
+      if (hi < tw) srcp0 = fit_src(a, bperm, 32 * (wave + FIT_NW * hi), nb, r32);
+      if (2 + hi < tw) srcp1 = fit_src(a, bperm, 32 * (wave + FIT_NW * (2 + hi)), nb, r32);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the index loads
+      if (tw > 0) fit_stage_pair(a, xs, srcp0, 0, Cin, lane);
+    }
     for (int i = 0; i < tw; ++i) {
       const int t = wave + FIT_NW * i;
       float* xt = xs + (onetile ? (s & 1) : (resident ? i : (i & 1))) * FIT_XT;
-      if (!onetile || s == 0) fit_stage(a, xt, bperm, 32 * t, nb, Cin, lane);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (onetile) {
+        if (s == 0) fit_stage(a, xt, bperm, 32 * t, nb, Cin, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (i + 1 < tw) {
+        fit_stage_pair(a, xs + (resident ? i + 1 : ((i + 1) & 1)) * FIT_XT, (i + 1) >= 2 ? srcp1 : srcp0,
+                       ((i + 1) & 1) * 32, Cin, lane);
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       f32x16 acc = forward(xt);
       uint32_t km;
       activate(acc, 32 * t, km);
@@ -456,9 +484,10 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
       // flight at once (one memory round trip when the partials are there), into ptab[gi][r]
       const uint64_t* part_in = a.part + (size_t)(s & 1) * G * a.bs * 3;
       const int Rp = ntile * 32, TPR = max(1, (FIT_NW * 64) / Rp);
-      const int part = tid / Rp, r = tid - part * Rp;
+      const int part = tid / Rp, r0 = tid - part * Rp;
       const int ngr = 3 * G;
-      if (part < TPR && r < nb) {
+      // batches beyond 256 rows: one part per thread, rows tid and tid + 256
+      for (int r = r0; part < TPR && r < nb; r += FIT_NW * 64) {
         for (int gi0 = part; gi0 < ngr; gi0 += TPR * FIT_POLL) {
           uint64_t gv[FIT_POLL];
           uint32_t pending = 0;
@@ -555,12 +584,19 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     // ---- pass 2: backward of this wave's tiles: dZ1, dW1 (MFMA), dW2, db1 ----
     f32x16 dw[3] = {f32x16{}, f32x16{}, f32x16{}};
     float dw2[3] = {0.f, 0.f, 0.f}, db1 = 0.f;
+    // batch > 256: the partial table overlaid the X slots, so the tiles are gathered again
+    // (pipelined as in pass 1) and their forward recomputed
+    if (!resident && tw > 0) fit_stage_pair(a, xs, srcp0, 0, Cin, lane);
     for (int i = 0; i < tw; ++i) {
       const int t = wave + FIT_NW * i;
       float* xt = xs + (onetile ? (s & 1) : (resident ? i : (i & 1))) * FIT_XT;
       if (!resident) {
-        fit_stage(a, xt, bperm, 32 * t, nb, Cin, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (i + 1 < tw) {
+          fit_stage_pair(a, xs + ((i + 1) & 1) * FIT_XT, (i + 1) >= 2 ? srcp1 : srcp0, ((i + 1) & 1) * 32, Cin, lane);
+          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
       f32x16 acc;
       uint32_t km;

@@ -18,6 +18,7 @@
 // HBM traffic per launch: the X rows once (+ labels, + the per-workgroup gradient slab).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "hpe_common.h"
 #include "hpe_dev.h"
@@ -653,6 +654,475 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   }
 }
 
+// ================================================================================================
+// mlp2w_kernel: the 12-wave fp16-split kernel (create_model with 128 < F <= 384: the headline
+// create_model(360)) with ONE workgroup barrier per 32-row tile instead of three.
+//   * X staging: waves 0..7 each own rows 4w .. 4w+3 of a tile (LDS-DMA into the single raw fp32
+//     buffer) and split exactly those rows into the tile's fp16 image (ch, cl, h fragments,
+//     row-major [32][96] with a per-row chunk rotation, wslot) after their OWN vmcnt(0): staging and
+//     splitting need no workgroup barrier.  The image serves both GEMMs: the forward reads rows
+//     (ds_read_b128), the dW1 GEMM reads X^T with the gfx950 transpose read ds_read_b64_tr_b16 —
+//     no second (transposed) copy.  Three images rotate: forward(t) / backward(t) / split(t+1).
+//   * tile t: forward(t) -> A1 parked in the wave's own LDS region, head partials -> part[t & 1];
+//     split X(t+1) (own rows) -> BARRIER -> stage X(t+2) -> head(t) computed by EVERY wave for all
+//     32 rows (12 partials per row summed in fixed wave order: bit-identical in every wave), its
+//     dZ2 written to the wave's own LDS row table -> backward(t) from the wave's own tables.
+//   * loss sums / db2 are accumulated by wave 0 only, in registers (no per-thread LDS table).
+// ================================================================================================
+#define W_FS 96                      // halves per row of a fragment image (12 chunks of 16 B)
+#define W_FRAG (32 * W_FS)           // halves per fragment image [32 rows][96]
+#define W_IMG (3 * W_FRAG)           // halves per tile image (ch, cl, h)
+#define W_NIMG 3                     // images in flight
+#define W_NLAB 3                     // label buffers in flight
+
+// slot of 16-byte chunk c (0..11) in row r: conflict-free for the forward row reads (ds_read_b128,
+// lanes = rows) and for the dW1 transposed reads (ds_read_b64_tr_b16, 4 rows x 4 chunks per half)
+__device__ __forceinline__ int wrot(int r) { return ((r >> 3) & 1) + 2 * (r >> 4); }
+__device__ __forceinline__ int wslot(int c, int rot) {
+  const int p = c + rot;
+  return p >= 12 ? p - 12 : p;
+}
+
+typedef __fp16 hf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h4 lds_tr16(const _Float16* p) {
+  const hf4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) hf4*)(uint32_t)(uintptr_t)p);
+  return __builtin_bit_cast(h4, v);
+}
+
+// LDS-DMA staging of rows 4w .. 4w+3 of a tile by wave w < 8 (labels by wave 0)
+__device__ __forceinline__ void w_stage(const Args& args, float* xs, float* lab, int64_t row0, const TileImg& ti,
+                                        int wave, int lane, int Cin, bool labels) {
+  if (wave >= 8) return;
+  const int64_t rem = args.nrows - 1 - row0;
+  const int last = rem < 31 ? (int)rem : 31;
+  const int P = args.P;
+  const int q = Cin >> 2;
+  if (!args.idx && P >= 32) {
+    if (labels && wave == 0) {
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int slot = pc * 64 + lane;
+        const int r = min(slot >> 2, last), j = min(slot & 3, 2);
+        glds4(args.ytrue + (int64_t)ti.of(r) * 3 + j, lds_addr(lab + pc * 64));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 4 * wave + k;
+      const int64_t srow = row0 + min(r, last);
+      if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
+    }
+    return;
+  }
+  const int lr = min(lane & 31, last);
+  const int limg = ti.of(lr);
+  const int lpos = (int)(row0 + lr - (int64_t)limg * P);
+  const int lsrc = args.idx ? args.idx[limg] : limg;
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (labels && wave == 0) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int slot = pc * 64 + lane;
+      const int r = min(slot >> 2, last), j = min(slot & 3, 2);
+      const int64_t src = __shfl(lsrc, r, 64);
+      glds4(args.ytrue + src * 3 + j, lds_addr(lab + pc * 64));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int rr = min(4 * wave + k, last);
+    const int64_t srow = (int64_t)__builtin_amdgcn_readlane(lsrc, rr) * P + __builtin_amdgcn_readlane(lpos, rr);
+    if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + (4 * wave + k) * MLP2_XS));
+  }
+}
+
+// split rows 4w .. 4w+3 of the landed raw tile into an image (wave w < 8): 4 rows x 24 f32x4
+template <int KH>
+__device__ __forceinline__ void w_split(const float* xs, _Float16* img, int wave, int lane) {
+  if (wave >= 8) return;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = lane + 64 * u;
+    if (i < 96) {
+      const int q = i / 24, rem = i - q * 24, h = rem >= 12 ? 1 : 0, m0 = 4 * (rem - 12 * h);
+      const int r = 4 * wave + q;
+      const f32x4 v = m0 < KH ? *(const f32x4*)(xs + r * MLP2_XS + KH * h + m0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      h4 ch, cl, hh;
+      split_d4(v, ch, cl, hh);
+      const int col = 48 * h + m0;
+      _Float16* d = img + r * W_FS + wslot(col >> 3, wrot(r)) * 8 + (col & 7);
+      *(h4*)(d) = ch;
+      *(h4*)(d + W_FRAG) = cl;
+      *(h4*)(d + 2 * W_FRAG) = hh;
+    }
+  }
+}
+
+__host__ __device__ constexpr int w_lds_floats(int ncb) {
+  return MLP2_XF + W_NLAB * MLP2_LAB + 2 * ncb * 32 * 4 + ncb * 32 * 4 + ncb * 1024 + ncb * 128 + 4 +
+         ncb * 128 + MLP2_RED + 32 * 8 + W_NIMG * W_IMG / 2;
+}
+
+template <int KH, int ACT1, bool DROP>
+__global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) mlp2w_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NKB = 3;
+  constexpr int T = 32;
+  const int* prog = args.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int mode = prog[H_MODE];
+  const bool train = mode == MODE_TRAIN;
+  const int Cin = o[O_K], F = o[O_N], NCB = o[O_MODE];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int n = wave * 32 + l32;
+  const bool nok = n < F;
+  float* xraw = lds;                              // [32][MLP2_XS] raw fp32 tile (LDS-DMA target)
+  float* lbuf = xraw + MLP2_XF;                   // [3][32][4] labels
+  float* part = lbuf + W_NLAB * MLP2_LAB;         // [2][NCB][32][4] head partials
+  float* dzp = part + 2 * NCB * T * 4;            // [NCB][32][4] per-wave dZ2 rows
+  float* a1s = dzp + NCB * T * 4;                 // [NCB][16][64] per-wave A1 park
+  float* w2t = a1s + NCB * 1024;                  // [NCB * 32][4]
+  float* b2t = w2t + NCB * 128;                   // [4]
+  float* colt = b2t + 4;                          // [NCB * 32][4] (inv1, b1, s2, -)
+  float* red = colt + NCB * 128;                  // [MLP2_RED]
+  float* hac = red + MLP2_RED;                    // [32][8] wave 0's per-row loss sums (sse, sae, db2[3])
+  _Float16* xf = (_Float16*)(hac + 32 * 8);       // [3 images][3 fragments][32][96]
+
+  E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
+  E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
+  const float inv_keep1 = 1.f / e1.keep;
+  const float* W1 = args.params + o[O_W];
+  const float* W2 = args.params + o[O_AUX0];
+
+  // register-resident W1 columns as split B fragments (as mlp2_kernel)
+  SplitW wsp[6];
+  float inv1, s2;
+  {
+    f32x8 v[6];
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = half * KH + 8 * s + j;
+        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
+        v[s][j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
+        mx = fmaxf(mx, fabsf(v[s][j]));
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float s1 = pow2_scale(mx, 13);
+    inv1 = SPLIT_INV_C / s1;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) wsp[s] = split_w8(v[s] * s1);
+    const float* w2n = args.params + o[O_AUX0] + min(n, F - 1) * 3;
+    s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
+    const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
+    if (half == 0) *(f32x4*)(colt + n * 4) = f32x4{inv1, b1, s2, 0.f};
+  }
+  for (int i = threadIdx.x; i < NCB * 128; i += blockDim.x) {
+    const int nn = i >> 2, j = i & 3;
+    w2t[i] = (nn < F && j < 3) ? W2[nn * 3 + j] : 0.f;
+  }
+  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
+
+  f32x16 dw[NKB];
+#pragma unroll
+  for (int s = 0; s < NKB; ++s) dw[s] = f32x16{};
+  float dw2[3] = {0.f, 0.f, 0.f};
+  float db1 = 0.f;
+  // wave 0, lanes 0..31: loss sums and db2 of its rows in LDS (the head is computed by every wave)
+  if (wave == 0 && half == 0) {
+    *(f32x4*)(hac + l32 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(hac + l32 * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bool bad = false;
+
+  const int64_t nrows = args.nrows;
+  const int ntiles = (int)((nrows + T - 1) / T);
+  const int P = args.P;
+  const bool labels = mode != MODE_FWD;
+  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = (int)(blockIdx.x * T / P);
+  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
+  // prologue: X(0) staged + split, barrier, X(1) staged
+  const int tile0 = blockIdx.x;
+  if (tile0 < ntiles) {
+    w_stage(args, xraw, lbuf, (int64_t)tile0 * T, ti, wave, lane, Cin, labels);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    w_split<KH>(xraw, xf, wave, lane);
+  }
+  __syncthreads();
+  TileImg tn = ti;
+  tn.advance(dq, dr);
+  if (tile0 + (int)gridDim.x < ntiles)
+    w_stage(args, xraw, lbuf + MLP2_LAB, (int64_t)(tile0 + gridDim.x) * T, tn, wave, lane, Cin, labels);
+
+  int it = 0;
+  for (int tile = tile0; tile < ntiles; tile += gridDim.x, ++it, ti.advance(dq, dr)) {
+    const int64_t row0 = (int64_t)tile * T;
+    const int im = it % 3;
+    const _Float16* img = xf + im * W_IMG;
+    float* pt = part + (it & 1) * NCB * T * 4;
+
+    // ---- forward(t): Z1 = X.W1 (+b1, act, dropout), A1 parked, head partials ----
+    uint32_t dmask = 0;
+    {
+      // per-lane read offsets recomputed per tile from an opaque copy of the lane id: hoisted out
+      // of the tile loop they would hold a dozen VGPRs across it (the kernel is at its budget)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int rot = wrot(ln & 31);
+      const _Float16* fp = img + (ln & 31) * W_FS;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const int off = wslot(6 * half + s, rot) * 8;
+        const SplitD xd = {*(const h8*)(fp + off), *(const h8*)(fp + W_FRAG + off), *(const h8*)(fp + 2 * W_FRAG + off)};
+        acc = mfma3_dw(xd, wsp[s], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
+      if (DROP) {
+        if (P >= 32) {
+          const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
+          const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << g) : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask |= drop_hash(args.seed, e1.drop, (uint64_t)(ti.of(r) + args.img_off), n) >= e1.thr ? (1u << g) : 0u;
+          }
+        }
+      }
+      const f32x4 cs = *(const f32x4*)(colt + n * 4);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        float z = act1_f<ACT1>(e1.act, fmaf(acc[g], cs.x, cs.y));
+        if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
+        acc[g] = nok ? z : 0.f;
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) a1s[(wave * 16 + g) * 64 + lane] = acc[g];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      {
+        const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
+        const float* ar = a1s + (wave * 16 + gr) * 64 + hh * 32 + 16 * half;
+        const float* wr = w2t + (wave * 32 + 16 * half) * 4;
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const f32x4 av = *(const f32x4*)(ar + i);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 w = *(const f32x4*)(wr + (i + e) * 4);
+            p0 = fmaf(av[e], w.x, p0);
+            p1 = fmaf(av[e], w.y, p1);
+            p2 = fmaf(av[e], w.z, p2);
+          }
+        }
+        p0 += xor32(p0);
+        p1 += xor32(p1);
+        p2 += xor32(p2);
+        if (half == 0) *(f32x4*)(pt + (wave * T + r) * 4) = f32x4{p0, p1, p2, 0.f};
+      }
+    }
+    // ---- split X(t+1) (own rows, after own pieces landed) ----
+    if (tile + (int)gridDim.x < ntiles) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      w_split<KH>(xraw, xf + ((it + 1) % 3) * W_IMG, wave, lane);
+    }
+    bar_lds();
+    // ---- stage X(t+2) into the raw buffer (free: every wave split X(t+1) before the barrier) ----
+    if (tile + 2 * (int)gridDim.x < ntiles) {
+      TileImg t2 = ti;
+      t2.advance(dq, dr);
+      t2.advance(dq, dr);
+      w_stage(args, xraw, lbuf + ((it + 2) % 3) * MLP2_LAB, (int64_t)(tile + 2 * gridDim.x) * T, t2, wave, lane,
+              Cin, labels);
+    }
+
+    // ---- head(t): every wave, all 32 rows (lane r, halves split the 12 partials) ----
+    {
+      const int r = l32;
+      f32x4 sp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+        const int w = 6 * half + u;
+        const f32x4 pv = w < NCB ? *(const f32x4*)(pt + (w * T + r) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        sp += pv;
+      }
+      f32x4 ot;
+      ot.x = xor32(sp.x);
+      ot.y = xor32(sp.y);
+      ot.z = xor32(sp.z);
+      const f32x4 zz = half ? ot + sp : sp + ot;  // (waves 0..5) + (waves 6..11) in every lane
+      const int64_t R = row0 + r;
+      const int64_t img64 = ti.of(r) + args.img_off;
+      const float* lab = lbuf + im * MLP2_LAB;
+      f32x4 gv = {0.f, 0.f, 0.f, 0.f};
+      float esq = 0.f, eab = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float z = zz[j] + b2t[j];
+        const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
+                                                         ? z / e2.keep : 0.f) : z)
+                                  : e_fwd(e2, args.seed, img64, j, z);
+        if (mode == MODE_FWD) {
+          if (wave == 0 && half == 0 && R < nrows) args.y[R * 3 + j] = p;
+        } else {
+          float g = 0.f;
+          if (R < nrows) {
+            const float err = p - lab[r * 4 + j];
+            esq = fmaf(err, err, esq);
+            eab += fabsf(err);
+            g = 2.f * err;
+          }
+          if (train) {
+            g = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
+                                                 ? g / e2.keep : 0.f) : g)
+                          : e_bwd(e2, args.seed, img64, j, g, p);
+          }
+          gv[j] = g;
+        }
+      }
+      if (wave == 0 && half == 0 && mode != MODE_FWD) {
+        f32x4 h0 = *(f32x4*)(hac + r * 8);
+        f32x4 h1 = *(f32x4*)(hac + r * 8 + 4);
+        h0.x += esq;
+        h0.y += eab;
+        h0.z += gv.x;
+        h0.w += gv.y;
+        h1.x += gv.z;
+        *(f32x4*)(hac + r * 8) = h0;
+        *(f32x4*)(hac + r * 8 + 4) = h1;
+      }
+      if (!train) continue;
+      if (half == 0) *(f32x4*)(dzp + (wave * T + r) * 4) = gv;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+
+    // ---- backward(t): dZ1 in registers, dW1 += X^T.dZ1 with X^T by transposed reads ----
+    {
+      const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
+      const float s2n = colt[n * 4 + 2];
+      auto dz_of = [&](int g) {
+        const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+        const f32x4 d = *(const f32x4*)(dzp + (wave * T + r) * 4);
+        const float a = a1s[(wave * 16 + g) * 64 + lane];
+        const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
+        float gz, av = a;
+        if (DROP) {
+          gz = (dmask >> g) & 1u ? da * inv_keep1 : 0.f;
+          av = a * e1.keep;
+        } else {
+          gz = da;
+        }
+        gz = nok ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
+        dw2[0] = fmaf(a, d.x, dw2[0]);
+        dw2[1] = fmaf(a, d.y, dw2[1]);
+        dw2[2] = fmaf(a, d.z, dw2[2]);
+        db1 += gz;
+        return gz;
+      };
+      // transposed reads: a group of 16 lanes covers 16 channels; lane 4q + p gives the address of
+      // row q (of 4), channels 4p .. 4p+3 (offsets from an opaque lane id, as in the forward)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int tq = (ln & 15) >> 2, tp = ln & 3;
+      const int tcc = 2 * ((ln >> 4) & 1) + (tp >> 1);     // chunk within a 32-channel block (0..3)
+      const int tbase = (4 * (ln >> 5) + tq) * W_FS + 4 * (tp & 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f32x8 dv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dv[j] = dz_of(8 * s + j);
+          if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        const SplitW dsp = split_w8(dv * s2n);
+        // rows 16 s + 4 h + q (elements 0..3) and 16 s + 8 + 4 h + q (4..7): rotations 2 s, 2 s + 1
+        const _Float16* ra = img + tbase + 16 * s * W_FS;
+        const _Float16* rb = ra + 8 * W_FS;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          const int oa = wslot(4 * kb + tcc, 2 * s) * 8, ob = wslot(4 * kb + tcc, 2 * s + 1) * 8;
+          SplitD xd;
+          xd.ch = __builtin_shufflevector(lds_tr16(ra + oa), lds_tr16(rb + ob), 0, 1, 2, 3, 4, 5, 6, 7);
+          xd.cl = __builtin_shufflevector(lds_tr16(ra + W_FRAG + oa), lds_tr16(rb + W_FRAG + ob), 0, 1, 2, 3, 4, 5, 6, 7);
+          xd.h = __builtin_shufflevector(lds_tr16(ra + 2 * W_FRAG + oa), lds_tr16(rb + 2 * W_FRAG + ob), 0, 1, 2, 3, 4, 5, 6, 7);
+          dw[kb] = mfma3_dw(xd, dsp, dw[kb]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+
+  if (mode == MODE_FWD) {
+    if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // ---- flush this workgroup's partial gradients + loss sums ----
+  const int slab = prog[H_SLAB];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  float* ws = args.ws + (size_t)blockIdx.x * slab;
+  const float sc = args.inv_count;
+  if (train) {
+    const float s2f = colt[n * 4 + 2];
+    float chk = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      chk += sum16(dw[kb]);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        // image position -> channel (KH = 44: positions 44..47 / 92..95 are padding)
+        const int kp = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        const int kh = kp >= 48 ? kp - 48 : kp;
+        const int k = (kp >= 48 ? KH : 0) + kh;
+        if (kh < KH && k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (sc * (SPLIT_INV_C / s2f));
+      }
+    }
+    bad |= !(fabsf(chk) <= 3.0e38f);
+    const float tb = db1 + __shfl_xor(db1, 32, 64);
+    float t2[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
+    if (half == 0 && nok) {
+      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
+    }
+  }
+  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0) {
+    const f32x4 h0 = half == 0 ? *(const f32x4*)(hac + l32 * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const float h1 = half == 0 ? hac[l32 * 8 + 4] : 0.f;
+    const float a = wave_sum(h0.x), b = wave_sum(h0.y);
+    const float d0 = wave_sum(h0.z), d1 = wave_sum(h0.w), d2 = wave_sum(h1);
+    if (lane == 0) {
+      ws[npt] = a;
+      ws[npt + 1] = b;
+      if (train && o[O_AUX1] >= 0) {
+        ws[o[O_AUX1] + 0] = d0 * sc;
+        ws[o[O_AUX1] + 1] = d1 * sc;
+        ws[o[O_AUX1] + 2] = d2 * sc;
+      }
+    }
+  }
+}
+
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
@@ -664,8 +1134,25 @@ static mlp2_fn pick_act(int act, int act2) {
   return mlp2_kernel<KH, -1, DROP, NWM, SPLIT>;
 }
 
+// the one-barrier 12-wave kernel (HPE_MLP2_1BAR=1): measured slower than mlp2_kernel so far
+static bool mlp2_one_barrier() {
+  const char* e = getenv("HPE_MLP2_1BAR");
+  return e && e[0] == '1';
+}
+template <int KH, bool DROP>
+static mlp2_fn pick_w(int act, int act2) {
+  if (act2 != ACT_LINEAR) return mlp2w_kernel<KH, -1, DROP>;
+  if (act == ACT_TANH) return mlp2w_kernel<KH, ACT_TANH, DROP>;
+  if (act == ACT_SOFTSIGN) return mlp2w_kernel<KH, ACT_SOFTSIGN, DROP>;
+  return mlp2w_kernel<KH, -1, DROP>;
+}
+
 template <bool DROP, bool SPLIT>
 static mlp2_fn pick_d(int kh, int act, int act2, int ncb) {
+  if (SPLIT && ncb > 4 && mlp2_one_barrier()) {  // the one-barrier 12-wave kernel
+    if (kh == 44) return pick_w<44, DROP>(act, act2);
+    if (kh == 48) return pick_w<48, DROP>(act, act2);
+  }
   if (ncb <= 4) {
     if (kh == 44) return pick_act<44, DROP, 4, SPLIT>(act, act2);  // 88-channel BlazeFace tap (Model-88)
     if (kh == 48) return pick_act<48, DROP, 4, SPLIT>(act, act2);  // 96-channel tap (Model-96)
@@ -700,6 +1187,14 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   if (ncb > 4 && pre > lds_bytes) lds_bytes = pre;
 }
 
+// LDS of the split instantiation pick(w, true) launches
+static int lds_split(const int* w) {
+  int kh, rbw, ncb, lds, act, drop;
+  geom(w, kh, rbw, ncb, lds, act, drop);
+  if (ncb > 4 && mlp2_one_barrier()) return w_lds_floats(ncb) * 4;
+  return lds;
+}
+
 static int launch_k(mlp2_fn k, int ncb, int lds, const Args& a, int grid, hipStream_t s) {
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   hipLaunchKernelGGL(k, dim3(grid), dim3(ncb * 64), lds, s, a);
@@ -716,7 +1211,7 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
     e.guard = nullptr;
     return launch_k(pick(w), ncb, lds, e, grid, s);
   }
-  if (launch_k(pick(w, true), ncb, lds, a, grid, s)) return 2;
+  if (launch_k(pick(w, true), ncb, lds_split(w), a, grid, s)) return 2;
   return launch_k(pick(w), ncb, lds, a, grid, s);
 }
 }  // namespace MLP2_NS
@@ -755,7 +1250,7 @@ static int per_cu_of(mlp2_fn k, int ncb, int lds) {
 int mlp2_grid_cap(const int* w, int n_cu) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
-  const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds);
+  const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds_split(w));
   return n_cu * (a < b ? a : b);
 }
 
