@@ -162,6 +162,7 @@ struct Args {
   int epoch;         //   -> the exact-fp32 kernel of the same launch re-runs (guard == epoch)
   float* gscr;       // rowprog_kernel<..., GS = true>: per-workgroup slot scratch (H_GSLOTS programs)
   int pass;          // rowprog_kernel: dW-block pass of a multi-pass (H_NPASS) training program
+  const float* wsplit;  // rowprog_kernel<..., SPLIT = true>: pre-split OP_DENSE weights (O_AUX3 offsets)
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -26,6 +26,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <vector>
+
 #include "hpe_prog.h"
 #include "../../include/hpe.h"
 
@@ -57,6 +59,107 @@ __device__ __forceinline__ void for_rc(int T, int C, F&& f) {
 // ds_read_b128; slot stride = 4*odd floats makes the 16-row lane groups conflict-free.
 // B[k][j=n] = W[k][n]: lanes 0-31 / 32-63 read one contiguous 128-B W row each (L2-resident).
 // ------------------------------------------------------------------------------------------------
+// SPLIT (inference programs): the weights were split by split_weights_kernel into the MFMA B
+// fragments of v_mfma_f32_32x32x16_f16 (hi / scaled-lo fp16, per-column power-of-two scale s1;
+// O_AUX3 = float offset in Args::wsplit: [ncb][nks][2][64 lanes x 8 halves], then [ncb * 32]
+// 1 / (C s1)); A = 8 consecutive k per lane half (two ds_read_b128), split in registers
+// (split_d8); 3 MFMAs (96 cycles) per 16 k instead of 8 exact-fp32 MFMAs (512 cycles), and one
+// 16-byte weight load per fragment instead of 16 scalar loads.  A non-finite accumulator (data
+// outside the split's range) sets *bad -> the exact-fp32 twin re-runs the launch.
+template <int NW>
+__device__ __forceinline__ void op_dense_split(const Ctx& c, const int* o, const float* wsplit, bool& bad) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
+  const int sa = o[O_A], so = o[O_OUT];
+  const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
+  const int o_off = slot_w(c, so, S_OFF), o_st = slot_w(c, so, S_STRIDE), o_cp = slot_w(c, so, S_CP);
+  const int K = o[O_K], N = o[O_N];
+  const int boff = o[O_BIAS];
+  const Epi e = load_epi(o);
+  const int nrb = c.T >> 5, ncb = (N + 31) >> 5, nks = (K + 15) >> 4;
+  const float* base = wsplit + o[O_AUX3];
+  const float* invs = base + (size_t)ncb * nks * 512;
+  for (int task = wave; task < nrb * ncb; task += NW) {
+    const int cb = task / nrb, rb = task - cb * nrb;
+    const int n = cb * 32 + l32;
+    const bool nok = n < N;
+    const float* ap = c.lds + a_off + (rb * 32 + l32) * a_st + 8 * half;
+    const h8* bp = (const h8*)(base + (size_t)cb * nks * 512) + lane;
+    f32x16 acc = {};
+    SplitW wn = {bp[0], bp[64]};
+    for (int s = 0; s < nks; ++s) {
+      const SplitW w = wn;
+      if (s + 1 < nks) wn = SplitW{bp[(s + 1) * 128], bp[(s + 1) * 128 + 64]};
+      const f32x4 a0 = *(const f32x4*)(ap + 16 * s), a1 = *(const f32x4*)(ap + 16 * s + 4);
+      acc = mfma3_dw(split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), w, acc);
+    }
+    bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
+    if (nok) {
+      const float inv = invs[n];
+      const float bv = boff >= 0 ? c.params[boff + n] : 0.f;
+      const int z_off = e.zslot >= 0 ? slot_w(c, e.zslot, S_OFF) : 0;
+      const int z_st = e.zslot >= 0 ? slot_w(c, e.zslot, S_STRIDE) : 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int r = rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        const float z = fmaf(acc[g], inv, bv);
+        c.lds[o_off + r * o_st + n] = epi_fwd(c, e, z, r, n);
+        if (e.zslot >= 0) c.lds[z_off + r * z_st + n] = z;
+      }
+    } else if (n < o_cp) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c.lds[o_off + (rb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * o_st + n] = 0.f;
+    }
+  }
+}
+
+// split_weights_kernel: one workgroup per (OP_DENSE op, 32-column block) of an inference program
+// (table: {op word offset, split float offset, column block}); the per-column scale from the
+// column's max |w| (pow2_scale, as mlp2), then the [nks][2][64][8] fragments of the block
+__global__ void __launch_bounds__(256) split_weights_kernel(const int* __restrict__ prog, const int* __restrict__ tab,
+                                                            const float* __restrict__ params,
+                                                            const float* __restrict__ params_t, float* __restrict__ wsplit) {
+  __shared__ float scale[32];
+  __shared__ float pmax[8][32];
+  const int* t = tab + 3 * blockIdx.x;
+  const int* o = prog + t[0];
+  const int cb = t[2];
+  const int K = o[O_K], N = o[O_N];
+  const float* W = (o[O_WSEL] ? params_t : params) + o[O_W];
+  const int ncb = (N + 31) >> 5, nks = (K + 15) >> 4;
+  float* base = wsplit + t[1];
+  {
+    // column max |w|: 8 k-groups x 32 columns, then a fixed-order combine
+    const int c = threadIdx.x & 31, kg = threadIdx.x >> 5, n = cb * 32 + c;
+    float mx = 0.f;
+    if (n < N)
+      for (int k = kg; k < K; k += 8) mx = fmaxf(mx, fabsf(W[(size_t)k * N + n]));
+    pmax[kg][c] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float mx = 0.f;
+    for (int kg = 0; kg < 8; ++kg) mx = fmaxf(mx, pmax[kg][threadIdx.x]);
+    const float s1 = pow2_scale(mx, 13);
+    scale[threadIdx.x] = s1;
+    if (cb * 32 + (int)threadIdx.x < ncb * 32) base[(size_t)ncb * nks * 512 + cb * 32 + threadIdx.x] = SPLIT_INV_C / s1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nks * 64; i += blockDim.x) {
+    const int s = i >> 6, lane = i & 63, l32 = lane & 31, h = lane >> 5;
+    const int n = cb * 32 + l32;
+    f32x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * h + j;
+      v[j] = (n < N && k < K) ? W[(size_t)k * N + n] * scale[l32] : 0.f;
+    }
+    const SplitW w = split_w8(v);
+    h8* d = (h8*)(base + ((size_t)cb * nks + s) * 512);
+    d[lane] = w.h;
+    d[64 + lane] = w.cl;
+  }
+}
+
 template <int NW>
 __device__ __forceinline__ void op_dense(const Ctx& c, const int* o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
@@ -166,6 +269,7 @@ __device__ __forceinline__ void op_tdense(const Ctx& c, const int* o) {
     const int k0 = s * kc, k1 = min(K, k0 + kc);
     const float* ap = c.lds + a_off + r * a_st;
     float acc = 0.f;
+#pragma unroll 8
     for (int k = k0; k < k1; ++k) acc = fmaf(ap[k], W[k * N + n], acc);
     scratch[it] = acc;
   }
@@ -226,38 +330,48 @@ __device__ __forceinline__ void op_ln(const Ctx& c, const int* o) {
   const float eps = __int_as_float(o[O_F0]);
   const Epi e = load_epi(o);
   const float invC = 1.f / (float)C;
+  // gamma / beta of this lane's channels loaded once per op (not once per row: the LDS stores in
+  // between keep the compiler from reusing global loads), DPP wave sums (no LDS round trips)
+  const int nj = (C + 63) >> 6;   // <= 8
+  float gam[8], bet[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ch = lane + 64 * j;
+    gam[j] = (j < nj && ch < C && goff >= 0) ? c.params[goff + ch] : 1.f;
+    bet[j] = (j < nj && ch < C && boff >= 0) ? c.params[boff + ch] : 0.f;
+  }
+  const int xs_off = xs >= 0 ? slot_w(c, xs, S_OFF) : 0, xs_st = xs >= 0 ? slot_w(c, xs, S_STRIDE) : 0;
+  const int rs_off = rs >= 0 ? slot_w(c, rs, S_OFF) : 0, rs_st = rs >= 0 ? slot_w(c, rs, S_STRIDE) : 0;
   for (int r = wave; r < c.T; r += NW) {
     float v[8];
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ch = lane + 64 * j;
-      v[j] = ch < C ? c.lds[a_off + r * a_st + ch] : 0.f;
+      v[j] = (j < nj && ch < C) ? c.lds[a_off + r * a_st + ch] : 0.f;
       s += v[j];
     }
-    const float mean = wave_sum(s) * invC;
+    const float mean = wave_sum_dpp(s) * invC;
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ch = lane + 64 * j;
-      const float d = ch < C ? v[j] - mean : 0.f;
+      const float d = (j < nj && ch < C) ? v[j] - mean : 0.f;
       q += d * d;
     }
-    const float var = wave_sum(q) * invC;
+    const float var = wave_sum_dpp(q) * invC;
     const float rstd = rsqrtf(var + eps);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ch = lane + 64 * j;
-      if (ch < C) {
+      if (j < nj && ch < C) {
         const float xh = (v[j] - mean) * rstd;
-        float y = xh;
-        if (goff >= 0) y *= c.params[goff + ch];
-        if (boff >= 0) y += c.params[boff + ch];
+        const float y = fmaf(xh, gam[j], bet[j]);
         c.lds[o_off + r * o_st + ch] = epi_fwd(c, e, y, r, ch);
-        if (xs >= 0) c.lds[slot_w(c, xs, S_OFF) + r * slot_w(c, xs, S_STRIDE) + ch] = xh;
+        if (xs >= 0) c.lds[xs_off + r * xs_st + ch] = xh;
       }
     }
-    if (rs >= 0 && lane == 0) c.lds[slot_w(c, rs, S_OFF) + r * slot_w(c, rs, S_STRIDE)] = rstd;
+    if (rs >= 0 && lane == 0) c.lds[rs_off + r * rs_st] = rstd;
   }
   zero_pads<NW>(c, o[O_OUT], C);
   if (xs >= 0) zero_pads<NW>(c, xs, C);
@@ -504,8 +618,10 @@ __device__ __forceinline__ void op_lnb(const Ctx& c, const int* o) {
 // more dW blocks than NW * MAXACC accumulators run H_NPASS launches, pass p owning blocks
 // [p NW MAXACC, (p+1) NW MAXACC) (the forward / backward is recomputed per pass; every other slab
 // entry is written with identical values by each pass).
-template <int NW, int MAXACC, bool GS>
+template <int NW, int MAXACC, bool GS, bool SPLIT = false>
 __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
+  // exact twin of a split launch: runs only when the split kernel flagged a non-finite value
+  if (!SPLIT && args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   constexpr int NT = NW * 64;
   const int* prog = args.prog;
@@ -540,6 +656,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
 #pragma unroll
   for (int s = 0; s < MAXTHIN; ++s) tacc[s] = 0.f;
   float sse = 0.f, sae = 0.f;
+  bool bad = false;
 
   const int in_off = slot_w(c, in_slot, S_OFF), in_st = slot_w(c, in_slot, S_STRIDE);
   const int64_t ntiles = (args.nrows + T - 1) / T;
@@ -584,7 +701,10 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
       const int* o = prog + ops_off + oi * O_WORDS;
       const int type = o[O_TYPE];
       switch (type) {
-        case OP_DENSE: op_dense<NW>(c, o); break;
+        case OP_DENSE:
+          if (SPLIT && o[O_AUX3] >= 0) op_dense_split<NW>(c, o, args.wsplit, bad);
+          else op_dense<NW>(c, o);
+          break;
         case OP_TDENSE: op_tdense<NW>(c, o); break;
         case OP_EW: op_ew<NW>(c, o); break;
         case OP_LN: op_ln<NW>(c, o); break;
@@ -665,7 +785,10 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     }
   }
 
-  if (mode == MODE_FWD) return;
+  if (mode == MODE_FWD) {
+    if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // ---- flush this workgroup's partials: slab[blockIdx] = [dW..., sum e^2, sum |e|] ----
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
@@ -816,6 +939,9 @@ struct hpe_program {
   int64_t n_words;
   mutable int epoch;  // guarded (fp16-split) launches: guard word = dwords[n_words + epoch % HPE_GUARD_RING]
   float* gscr;        // H_GSLOTS programs: grid_cap x H_LDS_FLOATS slot scratch
+  float* wsplit;      // inference programs: OP_DENSE weights split for the fp16 MFMA (null: exact only)
+  int* split_tab;     // device {op word offset, split offset, column block} per split workgroup
+  int n_split_blocks;
 };
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
@@ -847,6 +973,13 @@ static kfn_t pick_acc(int maxacc) {
   if (maxacc <= 2) return rowprog_kernel<NW, 2, GS>;
   if (maxacc <= 4) return rowprog_kernel<NW, 4, GS>;
   if (maxacc <= 8) return rowprog_kernel<NW, 8, GS>;
+  return nullptr;
+}
+
+// split instantiation: inference programs (MAXACC 1, LDS slots) on 8 waves
+static kfn_t pick_split(int nw, int maxacc) {
+  if (maxacc > 1) return nullptr;
+  if (nw == 8) return rowprog_kernel<8, 1, false, true>;   // (16 waves: spills at 128 VGPRs)
   return nullptr;
 }
 
@@ -889,11 +1022,43 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   p->n_words = n_words;
   p->epoch = 0;
   p->gscr = nullptr;
+  p->wsplit = nullptr;
+  p->split_tab = nullptr;
+  p->n_split_blocks = 0;
+  // inference programs of the generic interpreter: OP_DENSE ops get a split-weight region (device
+  // words O_AUX3), filled from the parameters by split_weights_kernel at every hpe_forward
+  std::vector<int> dw(words, words + n_words);
+  std::vector<int> tab;
+  int64_t nsplit = 0;
+  if (kind == KIND_GENERIC && words[H_MODE] == MODE_FWD && !words[H_GSLOTS]) {
+    for (int i = 0; i < words[H_NOPS]; ++i) {
+      const int wo = words[H_OPS_OFF] + i * O_WORDS;
+      if (words[wo + O_TYPE] != OP_DENSE) continue;
+      const int K = words[wo + O_K], N = words[wo + O_N];
+      const int ncb = (N + 31) >> 5, nks = (K + 15) >> 4;
+      dw[wo + O_AUX3] = (int)nsplit;
+      for (int cb = 0; cb < ncb; ++cb) {
+        tab.push_back(wo);
+        tab.push_back((int)nsplit);
+        tab.push_back(cb);
+      }
+      nsplit += (int64_t)ncb * nks * 512 + ncb * 32;
+    }
+  }
   hipError_t e = hipMalloc(&p->dwords, (n_words + HPE_GUARD_RING) * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
   e = hipMemset(p->dwords + n_words, 0, HPE_GUARD_RING * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMemcpy(p->dwords, words, n_words * sizeof(int32_t), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { hipFree(p->dwords); delete p; return fail(HPE_ERUNTIME, "hipMemcpy: %s", hipGetErrorString(e)); }
+  if (e == hipSuccess) e = hipMemcpy(p->dwords, dw.data(), n_words * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess && nsplit > 0) {
+    e = hipMalloc(&p->wsplit, nsplit * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&p->split_tab, tab.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(p->split_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice);
+    p->n_split_blocks = (int)(tab.size() / 3);
+  }
+  if (e != hipSuccess) {
+    hipFree(p->dwords); hipFree(p->wsplit); hipFree(p->split_tab); delete[] p->words; delete p;
+    return fail(HPE_ERUNTIME, "hipMalloc / hipMemcpy: %s", hipGetErrorString(e));
+  }
   int dev = 0;
   hipGetDevice(&dev);
   int ncu = 256;
@@ -920,6 +1085,14 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, (const void*)k, nw * 64, lds_bytes_of(words)) == hipSuccess &&
         res > 0 && res < per_cu)
       p->grid_cap = ncu * res;
+    kfn_t ks = p->wsplit ? pick_split(nw, words[H_MAXACC]) : nullptr;
+    if (ks) {
+      hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes_of(words));
+      res = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, (const void*)ks, nw * 64, lds_bytes_of(words)) == hipSuccess &&
+          res > 0 && ncu * res < p->grid_cap)
+        p->grid_cap = ncu * res;
+    }
 #endif
     if (gs) {
       e = hipMalloc(&p->gscr, (size_t)p->grid_cap * words[H_LDS_FLOATS] * sizeof(float));
@@ -937,6 +1110,8 @@ extern "C" int hpe_program_destroy(hpe_program* p) {
   if (!p) return HPE_OK;
   hipFree(p->dwords);
   if (p->gscr) hipFree(p->gscr);
+  if (p->wsplit) hipFree(p->wsplit);
+  if (p->split_tab) hipFree(p->split_tab);
   delete[] p->words;
   delete p;
   return HPE_OK;
@@ -977,6 +1152,21 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   }
   kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC], p->hdr[H_GSLOTS]);
   a.gscr = p->gscr;
+  kfn_t ks = p->wsplit && !hpe_exact_fp32() ? pick_split(p->hdr[H_NW], p->hdr[H_MAXACC]) : nullptr;
+  if (ks) {
+    // split the current weights (one workgroup per 32-column block), the split interpreter, then
+    // its exact-fp32 twin, which exits at once unless the split launch flagged a non-finite value
+    hipLaunchKernelGGL(split_weights_kernel, dim3(p->n_split_blocks), dim3(256), 0, s, (const int*)p->dwords,
+                       (const int*)p->split_tab, a.params, a.params_t, p->wsplit);
+    HIPCHK(hipGetLastError());
+    a.wsplit = p->wsplit;
+    hipLaunchKernelGGL(ks, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
+    HIPCHK(hipGetLastError());
+    return HPE_OK;
+  }
+  a.guard = nullptr;  // no split launch ahead: the kernel runs unconditionally
   const int npass = p->hdr[H_MODE] == MODE_TRAIN && p->hdr[H_NPASS] > 1 ? p->hdr[H_NPASS] : 1;
   for (int pass = 0; pass < npass; ++pass) {
     a.pass = pass;

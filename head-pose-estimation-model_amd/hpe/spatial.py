@@ -12,8 +12,9 @@ not row-local, so the graph is cut there and run as a staged pipeline, every sta
          LayerNorm + 1x1-conv regressor, the reference's own layers]--> (yaw, pitch, roll) rows
 
 Programs B and D are ordinary Keras graphs built here from the original layers and weights:
-B's kernel is [I | Wq/sqrt(d) | Wk | Wv]; D reads the [xg | o] row through two Dense layers,
-[I; 0] (the residual branch, exact in fp32) and [0; Wo] (named like the attention layer).  The
+B's kernel is [I | Wq/sqrt(d) | Wk | Wv]; D reads the [xg | o] row through ONE Dense layer with
+kernel [I; Wo] that stands for the residual Add(xg, attention output) (named like the Add; a
+graph that reads xg or the attention output elsewhere keeps two Dense layers, [I; 0] and [0; Wo]).  The
 Lambda flatten / reshape-back layers are identities on rows.  Forward (predict) only: the
 reference trains these heads on 1x1 maps (train_88.py:270-305).
 """
@@ -179,15 +180,30 @@ class SpatialPlan:
             self.qkv_config = _model('spatial_qkv', [_input('qkv_in', C), _dense('qkv', C + 3 * HD, ['qkv_in'])],
                                      'qkv_in', 'qkv')
             self.qkv_weights = {'qkv/kernel': kb, 'qkv/bias': bb}
-            # program D input: [xg | o]
-            sub_layers += [_input(sub_in, C + HD), _dense('spatial_residual', C, [sub_in]),
-                           _dense(nm, C, [sub_in])]
-            sub_w['spatial_residual/kernel'] = np.concatenate([np.eye(C, dtype=np.float32),
-                                                               np.zeros((HD, C), np.float32)])
-            sub_w['spatial_residual/bias'] = np.zeros(C, np.float32)
-            sub_w[nm + '/kernel'] = np.concatenate([np.zeros((C, C), np.float32), wo])
-            sub_w[nm + '/bias'] = bo
-            remap[xg] = 'spatial_residual'
+            # program D input: [xg | o].  The reference's residual Add(flat, attn) (attention_model.py:
+            # 56) reads exactly xg and the attention output, so it folds into ONE Dense with kernel
+            # [I; Wo] and bias bo (xg + (o Wo + bo) in one accumulation; no identity GEMM, no Add
+            # op); any other reader of xg / the attention output gets [I; 0] / [0; Wo] branches
+            res_add = [l for l in layers if l['class_name'] == 'Add' and
+                       sorted(canon(i) for i in l['ins']) == sorted([xg, nm])]
+            readers = [l for l in layers if l['name'] not in alias and
+                       any(canon(i) in (xg, nm) for i in l['ins']) and l['name'] not in
+                       {x['name'] for x in res_add} | {nm} | consumed]
+            sub_layers.append(_input(sub_in, C + HD))
+            if len(res_add) == 1 and not readers:
+                fused = res_add[0]['name']
+                sub_layers.append(_dense(fused, C, [sub_in]))
+                sub_w[fused + '/kernel'] = np.concatenate([np.eye(C, dtype=np.float32), wo])
+                sub_w[fused + '/bias'] = bo
+                consumed.add(fused)
+            else:
+                sub_layers += [_dense('spatial_residual', C, [sub_in]), _dense(nm, C, [sub_in])]
+                sub_w['spatial_residual/kernel'] = np.concatenate([np.eye(C, dtype=np.float32),
+                                                                   np.zeros((HD, C), np.float32)])
+                sub_w['spatial_residual/bias'] = np.zeros(C, np.float32)
+                sub_w[nm + '/kernel'] = np.concatenate([np.zeros((C, C), np.float32), wo])
+                sub_w[nm + '/bias'] = bo
+                remap[xg] = 'spatial_residual'
             consumed.add(nm)
             self.d_in = C + HD
         else:
