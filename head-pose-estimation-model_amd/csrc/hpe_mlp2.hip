@@ -1123,6 +1123,532 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
   }
 }
 
+// ================================================================================================
+// mlp2v_kernel: create_model with 128 < F <= 384 and C_in <= 96 (the headline create_model(360)) on
+// v_mfma_f32_16x16x32_f16 (the fp16 split of hpe_common.h at fp32 accuracy), 8 waves of 48 hidden
+// units, two per SIMD: a 256-register budget holds W1 (72 VGPRs of split B fragments), the dW1
+// accumulators (72) and a whole tile's Z1 (24) without spilling.  ONE workgroup barrier per
+// 32-row tile, and no phase in which most waves wait for a few (the 12-wave kernel runs three
+// lock-step phases per tile and a 96-item head on two waves).
+//   * staging (w_stage): wave w LDS-DMAs rows 4w .. 4w+3 of tile t+2 into the raw fp32 tile
+//     (labels: wave 0) and, one tile later, splits exactly those rows into the fp16 images after
+//     its own vmcnt(0) — staging and splitting need no workgroup barrier;
+//   * fp16 images (fragments ch, cl, h of split_d8 each), both read conflict-free by ds_read_b128:
+//       forward    xf[row][96]: the 16-B chunk c of row r at c ^ ((r >> 1) & 3);
+//       transposed xt[ch][32]:  in the dW1 GEMM's K order, position 8g + j <-> tile row
+//                  16 (j >> 2) + 4g + (j & 3) (the rows the forward accumulator of lane group g
+//                  holds), chunk g of channel ch at g ^ f((ch >> 2) & 3), f = {0, 2, 3, 1};
+//   * tile t: forward Z1 = X.W1 (2 row blocks x 3 column blocks x 3 K-steps, 3 MFMAs each), act,
+//     head partials over the wave's 48 units (in-lane over the 3 column blocks, then a DPP
+//     reduce-scatter over the 16 lanes of a row group) -> part[t & 1]; split X(t+1); BARRIER;
+//     stage X(t+2); head(t) by EVERY wave for all 32 rows (8 partials summed in fixed wave order:
+//     the same bits in every wave), dZ2 to the wave's own LDS table; backward: dZ1 in registers
+//     straight from the forward accumulators (lane group g's rows are the K slice 8g .. 8g+7 of
+//     the dW1 GEMM) as the B operand of dW1 += X^T.dZ1, A = X^T from xt.
+//   Scope: training launches with P >= 32 (at most two images per tile: the configs[3] / Model-96
+//   96x96 step, contiguous or gathered by fit); evaluation, forward and P < 32 launches keep
+//   mlp2_kernel (the branches they need cost this kernel registers it does not have).
+//   Hazards (one barrier): xf has 2 buffers, xt 3 (split(t+1) runs while slower waves may still
+//   read xt(t-1) in backward(t-1)), part 2, labels 4; the raw tile rows of wave w are only ever
+//   touched by wave w.
+// ================================================================================================
+#define V_NW 8                 // waves per workgroup (48 hidden units each: F <= 384)
+#define V_XS 96                // row stride (floats) of the raw tile: a wave's 4 rows are one 1.5 KB run
+#define V_FRAGF (32 * 96)      // halves per forward-image fragment [32 rows][96 channels]
+#define V_FRAGT (96 * 32)      // halves per transposed-image fragment [96 channels][32 positions]
+
+// forward image: halves offset of 16-B chunk c of row r
+__device__ __forceinline__ int vf_off(int r, int c) { return r * 96 + 8 * (c ^ ((r >> 1) & 3)); }
+// transposed image: halves offset of chunk g (positions 8g .. 8g+7) of channel ch
+__device__ __forceinline__ int vt_off(int ch, int g) { return ch * 32 + 8 * (g ^ ((0x78 >> (2 * ((ch >> 2) & 3))) & 3)); }
+
+__host__ __device__ constexpr int v_lds_floats() {
+  return 32 * V_XS + 4 * MLP2_LAB + 2 * V_NW * 32 * 4 + V_NW * 32 * 4 + 2 * V_NW * 48 * 4 + 4 +
+         V_NW * 4 * 48 * 4 + 32 * 8 + (2 * 3 * V_FRAGF + 3 * 3 * V_FRAGT) / 2;
+}
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// LDS-DMA staging of rows 4w .. 4w+3 of a tile by wave w (labels by wave 0); at P >= 32 a tile
+// spans at most two images, so a gathered batch (fit: args.idx) needs two uniform index loads per
+// tile, not one per row; rows past the end repeat the last row (their gradient is zero)
+__device__ __forceinline__ void v_stage(const Args& args, float* xs, float* lab, int64_t row0, const TileImg& ti,
+                                        int wave, int lane, int Cin) {
+  const int64_t rem = args.nrows - 1 - row0;
+  const int last = rem < 31 ? (int)rem : 31;
+  const int P = args.P;
+  int64_t s0 = ti.img0, s1 = ti.img0 + 1;
+  if (args.idx) {
+    const int nimg = (int)(args.nrows / P);
+    s0 = args.idx[ti.img0];
+    s1 = ti.img0 + 1 < nimg ? args.idx[ti.img0 + 1] : s0;
+  }
+  // lane id recomputed here (v_mbcnt), not carried: a loop-carried per-lane address spilled to
+  // scratch makes every piece below wait (vmcnt) for the pieces issued before it
+  int ln = __lane_id();
+  asm volatile("" : "+v"(ln));  // opaque: nothing derived from it is hoisted out of the tile loop
+  if (wave == 0) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int slot = pc * 64 + ln;
+      const int r = min(slot >> 2, last), j = min(slot & 3, 2);
+      glds4(args.ytrue + (ti.rem0 + r >= P ? s1 : s0) * 3 + j, lds_addr(lab + pc * 64));
+    }
+  }
+  const int t0 = ti.rem0 + 4 * wave;
+  if (Cin == 96 && 4 * wave + 3 <= last && (t0 + 3 < P || t0 >= P)) {
+    // the wave's 4 rows are one 1,536-B run in HBM and in the raw tile: two pieces, not four
+    // (each LDS-DMA issue costs ~100 cycles)
+    const float* src = args.x + (t0 >= P ? s1 * P + (t0 - P) : s0 * P + t0) * 96;
+    glds16(src + 4 * ln, lds_addr(xs + 4 * wave * V_XS));
+    if (ln < 32) glds16(src + 256 + 4 * ln, lds_addr(xs + 4 * wave * V_XS + 256));
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * wave + k;
+    const int t = ti.rem0 + min(r, last);
+    const int64_t srow = t >= P ? s1 * P + (t - P) : s0 * P + t;
+    if (ln < (Cin >> 2)) glds16(args.x + srow * Cin + 4 * ln, lds_addr(xs + r * V_XS));
+  }
+}
+
+// split rows 4w .. 4w+3 of the landed raw tile (wave w) into both images; lane l < 48 takes
+// channels 2l, 2l+1 (pad channels of the raw tile hold zeros)
+__device__ __forceinline__ void v_split(const float* xs, _Float16* xf, _Float16* xt, int wave) {
+  int lane = __lane_id();
+  asm volatile("" : "+v"(lane));  // recomputed per call, not a loop-carried (spillable) address
+  if (lane >= 48) return;
+  const int c0 = 2 * lane;
+  h2 ch[4], cl[4], hh[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * wave + q;
+    const float2 v = *(const float2*)(xs + r * V_XS + c0);
+    const float s0 = v.x * SPLIT_C, s1 = v.y * SPLIT_C;
+    ch[q] = h2{(_Float16)s0, (_Float16)s1};
+    cl[q] = h2{(_Float16)(s0 - (float)ch[q].x), (_Float16)(s1 - (float)ch[q].y)};
+    hh[q] = h2{(_Float16)v.x, (_Float16)v.y};
+    const int off = vf_off(r, c0 >> 3) + (c0 & 7);
+    *(h2*)(xf + off) = ch[q];
+    *(h2*)(xf + V_FRAGF + off) = cl[q];
+    *(h2*)(xf + 2 * V_FRAGF + off) = hh[q];
+  }
+  // rows 4w + q -> positions 8 (w & 3) + 4 (w >> 2) + q: half a chunk per channel
+  const int g = wave & 3, p = 4 * (wave >> 2);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int off = vt_off(c0 + e, g) + p;
+    *(h4*)(xt + off) = h4{ch[0][e], ch[1][e], ch[2][e], ch[3][e]};
+    *(h4*)(xt + V_FRAGT + off) = h4{cl[0][e], cl[1][e], cl[2][e], cl[3][e]};
+    *(h4*)(xt + 2 * V_FRAGT + off) = h4{hh[0][e], hh[1][e], hh[2][e], hh[3][e]};
+  }
+}
+
+// acc += C (D.W) on v_mfma_f32_16x16x32_f16, data fragments as A (rows), weights as B
+__device__ __forceinline__ f32x4 mfma3_16(const SplitD& d, const SplitW& w, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(d.cl, w.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(d.h, w.cl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(d.ch, w.h, acc, 0, 0, 0);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+template <int ACT1, bool DROP>
+__global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) mlp2v_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int T = 32;
+  const int* prog = args.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int Cin = o[O_K], F = o[O_N];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int lg = lane >> 4, lc = lane & 15;  // MFMA lane group (K slice / row quad), column in a block
+  float* xraw = lds;                         // [32][V_XS] raw fp32 tile (LDS-DMA target)
+  float* lbuf = xraw + 32 * V_XS;              // [4][32][4] labels
+  float* part = lbuf + 4 * MLP2_LAB;         // [2][V_NW][32][4] head partials
+  float* dzt = part + 2 * V_NW * T * 4;      // [V_NW][32][4] per-wave dZ2 rows
+  float* colt = dzt + V_NW * T * 4;          // [V_NW * 48][4] (inv1, b1, s2, -) per hidden unit
+  float* w2t = colt + V_NW * 48 * 4;         // [V_NW * 48][4] W2 rows (zero past F)
+  float* b2t = w2t + V_NW * 48 * 4;          // [4]
+  float* gacc = b2t + 4;                     // [V_NW][4 lane groups][48][4] (dW2 row, db1) partial sums
+  float* hac = gacc + V_NW * 4 * 48 * 4;     // [32][8] wave 0's per-row loss sums (sse, sae, db2[3])
+  _Float16* xf = (_Float16*)(hac + 32 * 8);  // [2][3][32][96]
+  _Float16* xt = xf + 2 * 3 * V_FRAGF;       // [3][3][96][32]
+
+  E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
+  E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
+  const float inv_keep1 = 1.f / e1.keep;
+  const float* W1 = args.params + o[O_W];
+  const float* W2 = args.params + o[O_AUX0];
+  const int n0 = wave * 48 + lc;  // hidden unit of column block nb: n0 + 16 nb
+
+  // ---- W1 columns as split B fragments: lane (g, c) of block nb holds column n0 + 16 nb, K
+  // elements 32 ks + 8 g + j; per-unit power-of-two scales as mlp2_kernel ----
+  SplitW wsp[3][3];  // [K-step][column block]
+#pragma unroll
+  for (int nb = 0; nb < 3; ++nb) {
+    const int n = n0 + 16 * nb;
+    const bool nok = n < F;
+    f32x8 v[3];
+    float mx = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * ks + 8 * lg + j;
+        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
+        v[ks][j] = (k < Cin && nok) ? wv : 0.f;
+        mx = fmaxf(mx, fabsf(v[ks][j]));
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, xor32(mx));
+    const float s1 = pow2_scale(mx, 13);
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) wsp[ks][nb] = split_w8(v[ks] * s1);
+    if (lg == 0) {
+      const float* w2n = W2 + min(n, F - 1) * 3;
+      const float s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
+      const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
+      *(f32x4*)(colt + n * 4) = f32x4{SPLIT_INV_C / s1, b1, s2, 0.f};
+      *(f32x4*)(w2t + n * 4) = nok ? f32x4{w2n[0], w2n[1], w2n[2], 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
+  // pad channels [C_in, 96) of the raw tile: never written by the staging, split into zeros
+  for (int i = threadIdx.x; i < 32 * 96; i += V_NW * 64) {
+    const int r = i / 96, c = i - r * 96;
+    if (c >= Cin) xraw[r * V_XS + c] = 0.f;
+  }
+
+  f32x4 dw[6][3];  // dW1 blocks [channel block][column block]
+#pragma unroll
+  for (int cb = 0; cb < 6; ++cb)
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) dw[cb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // dW2 / db1 partial sums per (lane group, unit) and wave 0's loss sums live in LDS, not in 17
+  // loop-carried VGPRs (the kernel sits at its 256-register budget)
+  float* gme = gacc + ((wave * 4 + lg) * 48 + lc) * 4;  // + 64 nb: this lane's (unit, group) slot
+#pragma unroll
+  for (int nb = 0; nb < 3; ++nb) *(f32x4*)(gme + 64 * nb) = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (wave == 0 && half == 0) {
+    *(f32x4*)(hac + l32 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(hac + l32 * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bool bad = false;
+
+  const int64_t nrows = args.nrows;
+  const int ntiles = (int)((nrows + T - 1) / T);
+  const int P = args.P;
+  const int G = gridDim.x;
+  const int S = G * T, dq = S / P, dr = S - dq * P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = (int)(blockIdx.x * T / P);
+  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
+  const int tile0 = blockIdx.x;
+  __syncthreads();  // pad zeros and the tables before any staging / split
+  if (tile0 < ntiles) {
+    v_stage(args, xraw, lbuf, (int64_t)tile0 * T, ti, wave, lane, Cin);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v_split(xraw, xf, xt, wave);
+  }
+  __syncthreads();
+  {
+    TileImg tn = ti;
+    tn.advance(dq, dr);
+    if (tile0 + G < ntiles) v_stage(args, xraw, lbuf + MLP2_LAB, (int64_t)(tile0 + G) * T, tn, wave, lane, Cin);
+  }
+
+#ifdef MLP2_STAMPS
+  uint32_t vph[8] = {};
+  uint64_t vprev = __builtin_amdgcn_s_memtime();
+#define VSTAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); vph[i] += (uint32_t)(t_ - vprev); vprev = t_; } while (0)
+#else
+#define VSTAMP(i) do {} while (0)
+#endif
+  int it = 0;
+  for (int tile = tile0; tile < ntiles; tile += G, ++it, ti.advance(dq, dr)) {
+    const int64_t row0 = (int64_t)tile * T;
+    const _Float16* fimg = xf + (it & 1) * 3 * V_FRAGF;
+    const _Float16* timg = xt + (it % 3) * 3 * V_FRAGT;
+    float* pt = part + (it & 1) * V_NW * T * 4;
+
+    // ---- forward(t): Z1 = X.W1 -> act (+ dropout) in the accumulators; rows 16 mb + 4 g + i ----
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int off = vf_off(16 * mb + lc, 4 * ks + lg);
+        const SplitD xd = {*(const h8*)(fimg + off), *(const h8*)(fimg + V_FRAGF + off), *(const h8*)(fimg + 2 * V_FRAGF + off)};
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) acc[mb][nb] = mfma3_16(xd, wsp[ks][nb], acc[mb][nb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    VSTAMP(0);
+    {
+      float chk = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) chk += (acc[mb][nb][0] + acc[mb][nb][1]) + (acc[mb][nb][2] + acc[mb][nb][3]);
+      bad |= !(fabsf(chk) <= 3.0e38f);
+    }
+    uint32_t dmask = 0;  // keep bit of (mb, nb, i): 12 mb + 4 nb + i
+    if (DROP) {
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) {
+        const int n = n0 + 16 * nb;
+        const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
+        const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * mb + 4 * lg + i;
+            dmask |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << (12 * mb + 4 * nb + i)) : 0u;
+          }
+      }
+    }
+    {
+      const f32x4 cs0 = *(const f32x4*)(colt + n0 * 4), cs1 = *(const f32x4*)(colt + (n0 + 16) * 4),
+                  cs2 = *(const f32x4*)(colt + (n0 + 32) * 4);
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) {
+          const f32x4 cs = nb == 0 ? cs0 : (nb == 1 ? cs1 : cs2);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float zp = fmaf(acc[mb][nb][i], cs.x, cs.y);
+            float z = ACT1 == ACT_TANH ? fast_tanh5(zp) : act1_f<ACT1>(e1.act, zp);
+            if (DROP) z = (dmask >> (12 * mb + 4 * nb + i)) & 1u ? z * inv_keep1 : 0.f;
+            // act(0) = 0 for the compiled-in activations: units past F (zero W1 column, b1, W2
+            // row) come out 0 without a mask
+            acc[mb][nb][i] = (ACT1 >= 0 || n0 + 16 * nb < F) ? z : 0.f;
+          }
+        }
+    }
+    // head partials of this wave's 48 units, one row block at a time: in-lane over the 3 column
+    // blocks (12 values (i, j)), then a DPP reduce-scatter over the 16 lanes c of a row group —
+    // row_half_mirror (c <-> c ^ 7) splits the row pairs, quad_perm xor 2 the rows of a pair,
+    // quad_perm xor 1 and row_ror:8 complete the sum; lane c ends with row 16 mb + 4 g +
+    // 2 ((c >> 2) & 1) + ((c >> 1) & 1), all three outputs
+    {
+      const f32x4 w0 = *(const f32x4*)(w2t + n0 * 4), w1 = *(const f32x4*)(w2t + (n0 + 16) * 4),
+                  w2 = *(const f32x4*)(w2t + (n0 + 32) * 4);
+      const bool b2 = lc & 4, b1 = lc & 2;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        float v[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            v[3 * i + j] = fmaf(acc[mb][2][i], w2[j], fmaf(acc[mb][1][i], w1[j], acc[mb][0][i] * w0[j]));
+        float t6[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const float keep = b2 ? v[6 + k] : v[k], send = b2 ? v[k] : v[6 + k];
+          t6[k] = keep + dppf<0x141>(send);
+        }
+        float s3[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const float keep = b1 ? t6[3 + j] : t6[j], send = b1 ? t6[j] : t6[3 + j];
+          s3[j] = keep + dppf<0x4E>(send);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          s3[j] += dppf<0xB1>(s3[j]);
+          s3[j] += dppf<0x128>(s3[j]);
+        }
+        const int rr = 16 * mb + 4 * lg + 2 * ((lc >> 2) & 1) + ((lc >> 1) & 1);
+        if ((lc & 9) == 0) *(f32x4*)(pt + (wave * T + rr) * 4) = f32x4{s3[0], s3[1], s3[2], 0.f};
+      }
+    }
+    VSTAMP(1);
+    // ---- split X(t+1) (own rows, after own pieces landed), then stage X(t+2) into the same raw
+    // rows (only this wave touches them; the split consumed its reads) before the barrier, so the
+    // LDS-DMA issue overlaps the wait; labels rotate over 4 buffers (head(t-1) may still read
+    // buffer t-1 in a slower wave) ----
+    if (tile + G < ntiles) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      v_split(xraw, xf + ((it + 1) & 1) * 3 * V_FRAGF, xt + ((it + 1) % 3) * 3 * V_FRAGT, wave);
+    }
+    VSTAMP(2);
+    if (tile + 2 * G < ntiles) {
+      TileImg t2 = ti;
+      t2.advance(dq, dr);
+      t2.advance(dq, dr);
+      v_stage(args, xraw, lbuf + ((it + 2) & 3) * MLP2_LAB, (int64_t)(tile + 2 * G) * T, t2, wave, lane, Cin);
+    }
+    VSTAMP(3);
+    bar_lds();
+    VSTAMP(4);
+    // ---- head(t): every wave, all 32 rows (lane r, halves take waves 0..3 / 4..7) ----
+    {
+      const int r = l32;
+      f32x4 sp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sp += *(const f32x4*)(pt + ((4 * half + u) * T + r) * 4);
+      f32x4 ot;
+      ot.x = xor32(sp.x);
+      ot.y = xor32(sp.y);
+      ot.z = xor32(sp.z);
+      ot.w = 0.f;
+      const f32x4 zz = half ? ot + sp : sp + ot;  // (waves 0..3) + (waves 4..7) in every lane
+      const int64_t R = row0 + r;
+      const int64_t img64 = ti.of(r) + args.img_off;
+      const float* lab = lbuf + (it & 3) * MLP2_LAB;
+      f32x4 gv = {0.f, 0.f, 0.f, 0.f};
+      float esq = 0.f, eab = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float z = zz[j] + b2t[j];
+        const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
+                                                         ? z / e2.keep : 0.f) : z)
+                                  : e_fwd(e2, args.seed, img64, j, z);
+        float g = 0.f;
+        if (R < nrows) {
+          const float err = p - lab[r * 4 + j];
+          esq = fmaf(err, err, esq);
+          eab += fabsf(err);
+          g = 2.f * err;
+        }
+        gv[j] = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
+                                                  ? g / e2.keep : 0.f) : g)
+                          : e_bwd(e2, args.seed, img64, j, g, p);
+      }
+      if (wave == 0 && half == 0) {
+        f32x4 h0 = *(f32x4*)(hac + r * 8);
+        f32x4 h1 = *(f32x4*)(hac + r * 8 + 4);
+        h0 += f32x4{esq, eab, gv.x, gv.y};
+        h1.x += gv.z;
+        *(f32x4*)(hac + r * 8) = h0;
+        *(f32x4*)(hac + r * 8 + 4) = h1;
+      }
+      if (half == 0) *(f32x4*)(dzt + (wave * T + r) * 4) = gv;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+
+    VSTAMP(5);
+    // ---- backward(t): dZ1 (K slice of lane group g) as the B operand of dW1 += X^T.dZ1 ----
+    {
+      // one column block at a time (its 8 rows' dZ2 re-read per block: held for all three they
+      // would pin 24 VGPRs through the phase that sets the kernel's register peak)
+      SplitW dsp[3];
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) {
+        const int n = n0 + 16 * nb;
+        const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
+        f32x8 dv;
+        f32x4 gsum = {0.f, 0.f, 0.f, 0.f};  // this tile's (dW2 row, db1) of the lane's 8 rows
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x4 d = *(const f32x4*)(dzt + (wave * T + 16 * mb + 4 * lg + i) * 4);
+            const float a = acc[mb][nb][i];
+            const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
+            float gz, av = a;
+            if (DROP) {
+              gz = (dmask >> (12 * mb + 4 * nb + i)) & 1u ? da * inv_keep1 : 0.f;
+              av = a * e1.keep;
+            } else {
+              gz = da;
+            }
+            gz = n < F ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
+            gsum += f32x4{a * d.x, a * d.y, a * d.z, gz};
+            dv[4 * mb + i] = gz;
+          }
+        *(f32x4*)(gme + 64 * nb) += gsum;
+        dsp[nb] = split_w8(dv * colt[n * 4 + 2]);
+        asm volatile("" ::: "memory");  // the next block re-reads dZ2 (no CSE across blocks)
+      }
+      VSTAMP(6);
+#pragma unroll
+      for (int cb = 0; cb < 6; ++cb) {
+        const int off = vt_off(16 * cb + lc, lg);
+        const SplitD xd = {*(const h8*)(timg + off), *(const h8*)(timg + V_FRAGT + off), *(const h8*)(timg + 2 * V_FRAGT + off)};
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) dw[cb][nb] = mfma3_16(xd, dsp[nb], dw[cb][nb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    VSTAMP(7);
+  }
+
+#ifdef MLP2_STAMPS
+  if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4))
+    printf("VSTAMP w%d fwdmfma %u act+part %u split %u bar %u stage %u head %u brows %u bmfma %u\n", wave, vph[0],
+           vph[1], vph[2], vph[3], vph[4], vph[5], vph[6], vph[7]);
+#endif
+  // ---- flush this workgroup's partial gradients + loss sums ----
+  const int slab = prog[H_SLAB];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  float* ws = args.ws + (size_t)blockIdx.x * slab;
+  const float sc = args.inv_count;
+  {
+    float chk = 0.f;
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) {
+      const int n = n0 + 16 * nb;
+      const float s2f = colt[n * 4 + 2];
+#pragma unroll
+      for (int cb = 0; cb < 6; ++cb) {
+        chk += (dw[cb][nb][0] + dw[cb][nb][1]) + (dw[cb][nb][2] + dw[cb][nb][3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 16 * cb + 4 * lg + i;
+          if (k < Cin && n < F) ws[o[O_W] + (size_t)k * F + n] = dw[cb][nb][i] * (sc * (SPLIT_INV_C / s2f));
+        }
+      }
+      const f32x4 gs = *(const f32x4*)(gme + 64 * nb);
+      float tb = gs.w + __shfl_xor(gs.w, 16, 64);
+      tb += xor32(tb);
+      float t2[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        t2[j] = gs[j] + __shfl_xor(gs[j], 16, 64);
+        t2[j] += xor32(t2[j]);
+      }
+      if (lg == 0 && n < F) {
+        if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
+      }
+    }
+    bad |= !(fabsf(chk) <= 3.0e38f);
+  }
+  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0) {
+    const f32x4 h0 = half == 0 ? *(const f32x4*)(hac + l32 * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const float h1 = half == 0 ? hac[l32 * 8 + 4] : 0.f;
+    const float a = wave_sum(h0.x), b = wave_sum(h0.y);
+    const float d0 = wave_sum(h0.z), d1 = wave_sum(h0.w), d2 = wave_sum(h1);
+    if (lane == 0) {
+      ws[npt] = a;
+      ws[npt + 1] = b;
+      if (o[O_AUX1] >= 0) {
+        ws[o[O_AUX1] + 0] = d0 * sc;
+        ws[o[O_AUX1] + 1] = d1 * sc;
+        ws[o[O_AUX1] + 2] = d2 * sc;
+      }
+    }
+  }
+}
+
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
@@ -1145,6 +1671,26 @@ static mlp2_fn pick_w(int act, int act2) {
   if (act == ACT_TANH) return mlp2w_kernel<KH, ACT_TANH, DROP>;
   if (act == ACT_SOFTSIGN) return mlp2w_kernel<KH, ACT_SOFTSIGN, DROP>;
   return mlp2w_kernel<KH, -1, DROP>;
+}
+
+// the 8-wave 16x16x32 kernel (mlp2v_kernel) for the split launches it covers; HPE_MLP2_V=0 keeps
+// the 12-wave mlp2_kernel (A/B)
+static bool mlp2_v_enabled() {
+  const char* e = getenv("HPE_MLP2_V");
+  return !(e && e[0] == '0');
+}
+static bool use_v(const int* w, const Args& a) {
+  const int* o = w + w[H_OPS_OFF];
+  const int ncb = o[O_MODE];
+  return mlp2_v_enabled() && !mlp2_one_barrier() && w[H_MODE] == MODE_TRAIN && a.P >= 32 &&
+         ncb > 4 && ncb <= MLP2_MAXW && o[O_K] <= 96;
+}
+template <bool DROP>
+static mlp2_fn pick_v(int act, int act2) {
+  if (act2 != ACT_LINEAR) return mlp2v_kernel<-1, DROP>;
+  if (act == ACT_TANH) return mlp2v_kernel<ACT_TANH, DROP>;
+  if (act == ACT_SOFTSIGN) return mlp2v_kernel<ACT_SOFTSIGN, DROP>;
+  return mlp2v_kernel<-1, DROP>;
 }
 
 template <bool DROP, bool SPLIT>
@@ -1195,9 +1741,9 @@ static int lds_split(const int* w) {
   return lds;
 }
 
-static int launch_k(mlp2_fn k, int ncb, int lds, const Args& a, int grid, hipStream_t s) {
+static int launch_k(mlp2_fn k, int nw, int lds, const Args& a, int grid, hipStream_t s) {
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(ncb * 64), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(nw * 64), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -1211,7 +1757,13 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
     e.guard = nullptr;
     return launch_k(pick(w), ncb, lds, e, grid, s);
   }
-  if (launch_k(pick(w, true), ncb, lds_split(w), a, grid, s)) return 2;
+  if (use_v(w, a)) {
+    const int* o = w + w[H_OPS_OFF];
+    const mlp2_fn kv = o[O_EDROP] >= 0 ? pick_v<true>(act, o[O_AUX2]) : pick_v<false>(act, o[O_AUX2]);
+    if (launch_k(kv, V_NW, v_lds_floats() * 4, a, grid, s)) return 2;
+  } else if (launch_k(pick(w, true), ncb, lds_split(w), a, grid, s)) {
+    return 2;
+  }
   return launch_k(pick(w), ncb, lds, a, grid, s);
 }
 }  // namespace MLP2_NS
@@ -1251,7 +1803,12 @@ int mlp2_grid_cap(const int* w, int n_cu) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
   const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds_split(w));
-  return n_cu * (a < b ? a : b);
+  int m = a < b ? a : b;
+  if (ncb > 4) {  // training launches may run mlp2v_kernel (LDS-bound to one workgroup per CU)
+    const int c = per_cu_of(pick_v<false>(ACT_TANH, ACT_LINEAR), V_NW, v_lds_floats() * 4);
+    m = m < c ? m : c;
+  }
+  return n_cu * m;
 }
 
 int mlp2_launch(const int* w, const Args& a, int grid, hipStream_t s) {

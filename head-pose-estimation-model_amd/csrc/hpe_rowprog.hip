@@ -26,6 +26,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "hpe_prog.h"
@@ -942,6 +943,12 @@ struct hpe_program {
   float* wsplit;      // inference programs: OP_DENSE weights split for the fp16 MFMA (null: exact only)
   int* split_tab;     // device {op word offset, split offset, column block} per split workgroup
   int n_split_blocks;
+  // gscr / wsplit are one buffer per program: a launch on another stream than the last one that
+  // used them waits for that launch (scr_done) instead of sharing the scratch with it
+  hipEvent_t scr_done;
+  hipStream_t scr_stream;
+  bool scr_used;
+  std::mutex scr_mu;
 };
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
@@ -1025,6 +1032,9 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   p->wsplit = nullptr;
   p->split_tab = nullptr;
   p->n_split_blocks = 0;
+  p->scr_done = nullptr;
+  p->scr_stream = nullptr;
+  p->scr_used = false;
   // inference programs of the generic interpreter: OP_DENSE ops get a split-weight region (device
   // words O_AUX3), filled from the parameters by split_weights_kernel at every hpe_forward
   std::vector<int> dw(words, words + n_words);
@@ -1112,6 +1122,7 @@ extern "C" int hpe_program_destroy(hpe_program* p) {
   if (p->gscr) hipFree(p->gscr);
   if (p->wsplit) hipFree(p->wsplit);
   if (p->split_tab) hipFree(p->split_tab);
+  if (p->scr_done) hipEventDestroy(p->scr_done);
   delete[] p->words;
   delete p;
   return HPE_OK;
@@ -1153,6 +1164,27 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC], p->hdr[H_GSLOTS]);
   a.gscr = p->gscr;
   kfn_t ks = p->wsplit && !hpe_exact_fp32() ? pick_split(p->hdr[H_NW], p->hdr[H_MAXACC]) : nullptr;
+  // the program's shared scratch (device-scratch tile slots, split weights): ordered after the
+  // previous launch that used it when that launch went to another stream
+  std::unique_lock<std::mutex> scr_lock(p->scr_mu, std::defer_lock);
+  const bool uses_scr = p->gscr || ks;
+  if (uses_scr) {
+    scr_lock.lock();
+    hpe_program* mp = const_cast<hpe_program*>(p);
+    if (!mp->scr_done) HIPCHK(hipEventCreateWithFlags(&mp->scr_done, hipEventDisableTiming));
+    if (mp->scr_used && mp->scr_stream != s) HIPCHK(hipStreamWaitEvent(s, mp->scr_done, 0));
+  }
+  struct ScrRecord {  // records scr_done on s once the launches below are queued
+    hpe_program* p;
+    hipStream_t s;
+    bool on;
+    ~ScrRecord() {
+      if (on && hipEventRecord(p->scr_done, s) == hipSuccess) {
+        p->scr_stream = s;
+        p->scr_used = true;
+      }
+    }
+  } scr_rec{const_cast<hpe_program*>(p), s, uses_scr};
   if (ks) {
     // split the current weights (one workgroup per 32-column block), the split interpreter, then
     // its exact-fp32 twin, which exits at once unless the split launch flagged a non-finite value

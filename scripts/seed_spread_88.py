@@ -11,6 +11,10 @@ BIWI_Test_Enlarged_features_88, where stoqa9pt scores 7.8100 / 3.4456 (BASELINE.
 BIWI_Train_Enlarged_features_88 (10,284 rows); the reference also concatenated
 BIWI_NoTrack_Enlarged_features_88, which is absent from the reference checkout.  One run per seed on
 this GPU through Model.fit (fused epoch launches).  Writes gpurun_out/seed_spread_88.json.
+
+`python scripts/seed_spread_88.py <seeds> steps` instead trains every seed for stoqa9pt's own
+770,868 SGD steps with EarlyStopping off (match the checkpoint's run length) and writes
+gpurun_out/seed_spread_88_steps.json.
 """
 import json
 import os
@@ -70,7 +74,7 @@ def load(name):
     return d['features'].reshape(-1, 1, 1, 88).astype(np.float32), d['poses'].reshape(-1, 1, 1, 3)
 
 
-def main(seeds, max_epochs):
+def main(seeds, max_epochs, match_steps=False):
     import hpe
     from hpe import keras
     from hpe.data import train_test_split
@@ -84,10 +88,12 @@ def main(seeds, max_epochs):
         hpe.set_seed(s)
         keras.backend.clear_session()
         m = create_model(keras)
-        es = keras.callbacks.EarlyStopping(monitor='val_loss', patience=40, min_delta=0.001,
-                                           restore_best_weights=True)
+        cbs = [Progress()]
+        if not match_steps:
+            cbs.insert(0, keras.callbacks.EarlyStopping(monitor='val_loss', patience=40, min_delta=0.001,
+                                                        restore_best_weights=True))
         t0 = time.perf_counter()
-        h = m.fit(tx, ty, epochs=max_epochs, batch_size=128, validation_data=(vx, vy), callbacks=[es, Progress()], verbose=0)
+        h = m.fit(tx, ty, epochs=max_epochs, batch_size=128, validation_data=(vx, vy), callbacks=cbs, verbose=0)
         dt = time.perf_counter() - t0
         _, a_mae = m.evaluate(ax, ay, verbose=0)
         _, b_mae = m.evaluate(bx, by, verbose=0)
@@ -106,13 +112,21 @@ def main(seeds, max_epochs):
                    'MAE vs the reference checkpoint stoqa9pt -- parity unpinned',
            'reference_stoqa9pt': {'aflw2000_enlarged_mae': 7.8100, 'biwi_test_enlarged_mae': 3.4456, 'sgd_steps': 770868},
            'runs': runs, 'max_epochs': max_epochs,
+           'early_stopping': not match_steps,
            'aflw2000_enlarged_mae_mean': float(a.mean()), 'aflw2000_enlarged_mae_std': float(a.std(ddof=1)) if len(a) > 1 else 0.0,
            'biwi_test_enlarged_mae_mean': float(b.mean()), 'biwi_test_enlarged_mae_std': float(b.std(ddof=1)) if len(b) > 1 else 0.0}
-    with open(os.path.join(ROOT, 'gpurun_out', 'seed_spread_88.json'), 'w') as fh:
+    name = 'seed_spread_88_steps.json' if match_steps else 'seed_spread_88.json'
+    with open(os.path.join(ROOT, 'gpurun_out', name), 'w') as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != 'runs'}), flush=True)
 
 
+STOQA9PT_STEPS = 770868
+
 if __name__ == '__main__':
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    main(list(range(n)), int(sys.argv[2]) if len(sys.argv) > 2 else 15000)
+    if len(sys.argv) > 2 and sys.argv[2] == 'steps':
+        # 8,227 training rows -> 65 steps per epoch at batch 128
+        main(list(range(n)), -(-STOQA9PT_STEPS // 65), match_steps=True)
+    else:
+        main(list(range(n)), int(sys.argv[2]) if len(sys.argv) > 2 else 15000)

@@ -110,6 +110,26 @@ def test_blazeface_forward_matches_oracle(rid, n):
 
 
 @pytest.mark.gpu
+def test_blazeface_batch_1024_sampled_oracle():
+    """configs[4]'s batch (1,024 frames, blazeFaceDetectorH5.py:272): the persistent bf_direct /
+    bf_rows grids run a different number of tasks per workgroup than at <= 33 frames.  Frames are
+    independent, so 24 frames sampled across the batch (both ends, a stride through the middle)
+    are checked against the oracle on those frames alone, and the whole batch against a second
+    GPU run of the same frames in smaller batches (bit-identical: no cross-frame state)."""
+    mc, w = fixture(RID)
+    bf = B.BlazeFace(mc, w)
+    x = _images(1024, seed=1024)
+    got = bf.predict(x)
+    pick = np.concatenate([np.arange(4), np.linspace(10, 1010, 16).astype(int), np.arange(1020, 1024)])
+    ref = [o.detach().numpy() for o in K.Graph(mc, w).forward(x[pick])]
+    for o, g, r in zip(bf.structure['outputs'], got, ref):
+        np.testing.assert_allclose(g[pick], r, rtol=BF_RTOL, atol=BF_ATOL, err_msg=o)
+    parts = [bf.predict(x[i:i + 100]) for i in range(0, 1024, 100)]
+    for k, o in enumerate(bf.structure['outputs']):
+        np.testing.assert_array_equal(got[k], np.concatenate([p[k] for p in parts]), err_msg=o)
+
+
+@pytest.mark.gpu
 def test_blazeface_taps_match_oracle():
     import torch
     mc, w = fixture(RID)

@@ -291,6 +291,51 @@ def test_train_step_split_vs_exact_and_guard(rid, P):
     np.testing.assert_array_equal(go, go_exact)
 
 
+@pytest.mark.parametrize('F,act,dropout,side,n', [(360, 'tanh', 0.0, 96, 2), (360, 'tanh', 0.3, 8, 40),
+                                                  (200, 'elu', 0.2, 6, 50), (256, 'relu', 0.1, 12, 20),
+                                                  (137, 'softsign', 0.0, 33, 3)])
+def test_train_step_8wave_kernel(F, act, dropout, side, n):
+    """csrc/hpe_mlp2.hip mlp2v_kernel (contiguous training launches at P >= 32, 128 < F <= 384:
+    8 waves x 48 units on v_mfma_f32_16x16x32_f16, one barrier per tile, DPP head partials):
+    the gradient (incl. loss sums) against the exact-fp32 12-wave kernel and the float64 oracle,
+    for the compiled-in tanh / softsign, the runtime-activation instantiation (elu, relu) and
+    SpatialDropout on both layers; ragged row counts (n P not a multiple of the 32-row tile)."""
+    from hpe import _lib
+    hpe.set_seed(F)
+    m = _create_model(F, act, dropout, 0.1)
+    mc, w = m.model_config, m.weights_dict()
+    eng = m._eng()
+    P = side * side
+    assert eng.program('train', P).prog.kind == 'mlp2'
+    x = features(n, 96, seed=F + 7, h=side, w=side)
+    y = labels(n, seed=F + 8)
+    xt = torch.from_numpy(x.reshape(n * P, 96)).cuda()
+    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
+    inv = 1.0 / (n * P * 3)
+
+    def grad():
+        return eng.gradient(xt, yt, P, None, n, inv, seed=5).cpu().numpy().copy()
+
+    lib = _lib.load()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        g_exact = grad()
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    g_split = grad()
+    npt = eng.n_train
+    g64 = _data_grad64(mc, w, x, y, eng.layout, 5)
+    scale = np.abs(g64).max()
+    e_exact = np.abs(g_exact[:npt] - g64).max() / scale
+    e_split = np.abs(g_split[:npt] - g64).max() / scale
+    d = np.abs(g_split[:npt] - g_exact[:npt]).max() / scale
+    print('F=%d %s drop %.2f P=%d: vs float64 exact %.2e split %.2e; |split - exact| / max|g| = %.2e'
+          % (F, act, dropout, P, e_exact, e_split, d))
+    assert e_split <= 4 * e_exact + 2.0 ** -24, (e_split, e_exact)
+    assert d <= 1e-6, d
+    np.testing.assert_allclose(g_split[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
+
+
 def _create_model(F, act, dropout, l2, lr=2.8e-4):
     """train_96.py:65-110 create_model with the given width / activation / rates."""
     keras.backend.clear_session()
@@ -307,11 +352,13 @@ def _create_model(F, act, dropout, l2, lr=2.8e-4):
 
 
 @pytest.mark.parametrize('F,act,dropout,P', [(360, 'tanh', 0.05, 1), (360, 'tanh', 0.3, 16),
-                                             (256, 'relu', 0.1, 1), (200, 'elu', 0.2, 4)])
+                                             (256, 'relu', 0.1, 1), (200, 'elu', 0.2, 4),
+                                             (360, 'tanh', 0.3, 64), (200, 'elu', 0.2, 36)])
 def test_training_trajectory_wide_dropout(F, act, dropout, P):
     """the 12-wave split kernel (129 <= F <= 384) with dropout on both layers (the
     sweep.yaml grid: filters 256 / 360, dropout > 0), for the compiled-in tanh and the runtime
-    activation instantiation (ACT1 = -1), against the oracle's fit with the same dropout masks."""
+    activation instantiation (ACT1 = -1), against the oracle's fit with the same dropout masks;
+    at P >= 32 fit's gathered batches run the 8-wave mlp2v_kernel (two index loads per tile)."""
     hpe.set_seed(11)
     m = _create_model(F, act, dropout, 0.1)
     w0 = m.weights_dict()
