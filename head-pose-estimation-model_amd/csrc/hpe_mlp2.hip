@@ -1545,8 +1545,10 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
     VSTAMP(5);
     // ---- backward(t): dZ1 (K slice of lane group g) as the B operand of dW1 += X^T.dZ1 ----
     {
-      // one column block at a time (its 8 rows' dZ2 re-read per block: held for all three they
-      // would pin 24 VGPRs through the phase that sets the kernel's register peak)
+      // one column block at a time: its 8 rows' dZ2 re-read per block through an opaque zero offset
+      // (no CSE across blocks: held for all three they would pin 32 VGPRs through the phase that
+      // sets the kernel's register peak), which the scheduler may still issue early (3.45 -> 3.34 ms
+      // against a full memory clobber between blocks)
       SplitW dsp[3];
 #pragma unroll
       for (int nb = 0; nb < 3; ++nb) {
@@ -1554,11 +1556,13 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
         const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
         f32x8 dv;
         f32x4 gsum = {0.f, 0.f, 0.f, 0.f};  // this tile's (dW2 row, db1) of the lane's 8 rows
+        int zo = 0;
+        asm volatile("" : "+v"(zo));
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const f32x4 d = *(const f32x4*)(dzt + (wave * T + 16 * mb + 4 * lg + i) * 4);
+            const f32x4 d = *(const f32x4*)(dzt + zo + (wave * T + 16 * mb + 4 * lg + i) * 4);
             const float a = acc[mb][nb][i];
             const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
             float gz, av = a;
@@ -1574,7 +1578,6 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
           }
         *(f32x4*)(gme + 64 * nb) += gsum;
         dsp[nb] = split_w8(dv * colt[n * 4 + 2]);
-        asm volatile("" ::: "memory");  // the next block re-reads dZ2 (no CSE across blocks)
       }
       VSTAMP(6);
 #pragma unroll

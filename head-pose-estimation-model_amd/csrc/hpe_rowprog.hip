@@ -945,10 +945,10 @@ struct hpe_program {
   int n_split_blocks;
   // gscr / wsplit are one buffer per program: a launch on another stream than the last one that
   // used them waits for that launch (scr_done) instead of sharing the scratch with it
-  hipEvent_t scr_done;
-  hipStream_t scr_stream;
-  bool scr_used;
-  std::mutex scr_mu;
+  mutable hipEvent_t scr_done;
+  mutable hipStream_t scr_stream;
+  mutable bool scr_used;
+  mutable std::mutex scr_mu;
 };
 
 extern "C" const char* hpe_last_error(void) { return g_err; }
@@ -1170,12 +1170,11 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
   const bool uses_scr = p->gscr || ks;
   if (uses_scr) {
     scr_lock.lock();
-    hpe_program* mp = const_cast<hpe_program*>(p);
-    if (!mp->scr_done) HIPCHK(hipEventCreateWithFlags(&mp->scr_done, hipEventDisableTiming));
-    if (mp->scr_used && mp->scr_stream != s) HIPCHK(hipStreamWaitEvent(s, mp->scr_done, 0));
+    if (!p->scr_done) HIPCHK(hipEventCreateWithFlags(&p->scr_done, hipEventDisableTiming));
+    if (p->scr_used && p->scr_stream != s) HIPCHK(hipStreamWaitEvent(s, p->scr_done, 0));
   }
   struct ScrRecord {  // records scr_done on s once the launches below are queued
-    hpe_program* p;
+    const hpe_program* p;
     hipStream_t s;
     bool on;
     ~ScrRecord() {
@@ -1184,7 +1183,7 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
         p->scr_used = true;
       }
     }
-  } scr_rec{const_cast<hpe_program*>(p), s, uses_scr};
+  } scr_rec{p, s, uses_scr};
   if (ks) {
     // split the current weights (one workgroup per 32-column block), the split interpreter, then
     // its exact-fp32 twin, which exits at once unless the split launch flagged a non-finite value
