@@ -192,10 +192,21 @@ class Engine:
         return _lib.load().hpe_optim_grid(self.n_train)
 
     # -- whole-epoch launch (P = 1, one rank): csrc/hpe_fit.hip ----------------------------------
+    # batches above this run the per-step path unless HPE_FIT_FUSED=1: the epoch kernel computes
+    # on one XCD's workgroups (hidden units split over <= 32 CUs), which wins while a step is
+    # latency-bound (b128: 16.5 vs 41.7 us / step) and loses once it is not (b512: 56.1 vs 46.2 us,
+    # profiles/r03c_bench.json p1 lines, MI355X)
+    FIT_FUSED_AUTO_MAX = 256
+
     def fit_epoch_supported(self, batch, P=1, world=1):
         """True when fit's epoch can run as ONE hpe_fit_epoch launch: the reference's regime (1x1
-        maps, the 2-layer create_model family, one rank); HPE_FIT_FUSED=0 forces the per-step path."""
-        if world != 1 or P != 1 or os.environ.get('HPE_FIT_FUSED', '1') == '0':
+        maps, the 2-layer create_model family, one rank) at batch <= FIT_FUSED_AUTO_MAX;
+        HPE_FIT_FUSED=0 forces the per-step path, HPE_FIT_FUSED=1 the fused one wherever the
+        kernel supports the batch (<= 512)."""
+        env = os.environ.get('HPE_FIT_FUSED')
+        if world != 1 or P != 1 or env == '0':
+            return False
+        if env is None and batch > self.FIT_FUSED_AUTO_MAX:
             return False
         if getattr(self, '_fit_disabled', False):   # an earlier epoch launch timed out
             return False

@@ -203,6 +203,25 @@ def summarize_line(tag, line, steps=10, warmup=2, pmc_steps=5, pmc_warmup=1):
     return res
 
 
+def profiled_step_ms(tag, line):
+    """the bench line's own ms per step / batch as printed by the PROFILED process itself
+    (gpurun_out/prof_<tag>_<line>.log): the like-for-like bound for the trace average (a separate
+    un-profiled bench run clocks higher)"""
+    p = os.path.join(OUT, 'prof_%s_%s.log' % (tag, line))
+    if not os.path.exists(p):
+        return None
+    for ln in open(p):
+        if ln.startswith('{'):
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                continue
+            v = d if line == 'train' else d.get(line, {})
+            if isinstance(v, dict):
+                return v.get('ms_per_step', v.get('ms_per_batch'))
+    return None
+
+
 def main(tag, lines, steps=10, warmup=2):
     os.makedirs(PROF, exist_ok=True)
     path = os.path.join(PROF, 'traffic.json')
@@ -217,6 +236,9 @@ def main(tag, lines, steps=10, warmup=2):
         if r:
             r['source'] = ('profiles/%s_%s_kernel_stats_timed.csv (timed-region dispatches of %s_%s_kernel_'
                            'stats.csv), %s_%s_pmc.csv' % (tag, line, tag, line, tag, line))
+            ms = profiled_step_ms(tag, line)
+            if ms is not None:
+                r['profiled_process_ms_per_step'] = ms
             out[line] = r
     out['tag'] = tag
     out['note'] = ('per bench line, profiled in its own process (bench.py --only <line> --steps %d --warmup %d); '

@@ -405,3 +405,42 @@ def test_configs2_biwi_train_88_adam_b512():
         np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
     np.testing.assert_allclose(hist.history['val_loss'], vlosses, rtol=1e-4)
     assert np.isfinite(hist.history['loss']).all() and hist.history['loss'][-1] < hist.history['loss'][0]
+
+
+def test_train_88_default_complex_on_biwi_enlarged():
+    """train_88.py's own default graph: create_model_complex(1e-6, 1e-4)
+    (Model-88/attention_model.py:97-169 -> the drop-in builder), legacy SGD lr 2.8e-4, batch 128
+    (train_88.py:48,53,323,355-363), on the reference's training data BIWI_Train_Enlarged_features_88
+    (the first 1,000 rows after train_test_split(0.2, 42), 8 steps per epoch, last batch partial),
+    2 epochs in order, against the float64 oracle's fit on the same rows (dropout masks by the same
+    counter hash): every weight within rtol 2e-4 / atol 2e-5."""
+    import importlib.util
+    import os
+    from hpe.data import train_test_split
+    d = np.load(DATA + '/BIWI_Train_Enlarged_features_88_0.7_1.npz')
+    x = d['features'].reshape(-1, 1, 1, 88).astype(np.float32)
+    y = d['poses'].reshape(-1, 1, 1, 3)
+    tx, _, ty, _ = train_test_split(x, y, test_size=0.2, random_state=42)
+    tx, ty = tx[:1000], ty[:1000]
+    path = os.path.join(os.path.dirname(DATA), '..', '..', 'head-pose-estimation-model_amd', 'Model-88',
+                        'attention_model.py')
+    spec = importlib.util.spec_from_file_location('hpe_attention_model_88_t', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    keras.backend.clear_session()
+    hpe.set_seed(88)
+    m = mod.create_model_complex(1e-6, 1e-4)
+    m.compile(optimizer=keras.optimizers.SGD(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    w0 = m.weights_dict()
+    hist = m.fit(tx, ty, batch_size=128, epochs=2, shuffle=False, verbose=0)
+    g = K.Graph(m.model_config, w0)
+    o = K.LegacyOptimizer('sgd', 2.8e-4)
+    it = 0
+    for _ in range(2):
+        for b0 in range(0, tx.shape[0], 128):
+            it += 1
+            K.train_step(g, o, tx[b0:b0 + 128], ty[b0:b0 + 128].reshape(-1, 3), drop_seed=hpe.random.dropout_seed(it))
+    got = m.weights_dict()
+    for k in g.trainable:
+        np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
+    assert np.isfinite(hist.history['loss']).all()
