@@ -1130,9 +1130,12 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
 // accumulators (72) and a whole tile's Z1 (24) without spilling.  ONE workgroup barrier per
 // 32-row tile, and no phase in which most waves wait for a few (the 12-wave kernel runs three
 // lock-step phases per tile and a 96-item head on two waves).
-//   * staging (w_stage): wave w LDS-DMAs rows 4w .. 4w+3 of tile t+2 into the raw fp32 tile
-//     (labels: wave 0) and, one tile later, splits exactly those rows into the fp16 images after
-//     its own vmcnt(0) — staging and splitting need no workgroup barrier;
+//   * staging (v_stage): wave w LDS-DMAs rows 4w .. 4w+3 of tile t+2 into the raw fp32 tile
+//     (labels: wave 0) after its backward rows of tile t and, one tile later, splits exactly those
+//     rows into the fp16 images after its own vmcnt(0) (an LDS-DMA is ordered for the issuing
+//     wave's ds_read by its vmcnt alone) — staging and splitting need no workgroup barrier.  No DMA
+//     is in flight while the head / backward rows run their LDS read-modify-writes: issued before
+//     the barrier (across them), 1-18 % of launches lost a dW2 partial (race screens on MI355X);
 //   * fp16 images (fragments ch, cl, h of split_d8 each), both read conflict-free by ds_read_b128:
 //       forward    xf[row][96]: the 16-B chunk c of row r at c ^ ((r >> 1) & 3);
 //       transposed xt[ch][32]:  in the dW1 GEMM's K order, position 8g + j <-> tile row
@@ -1141,10 +1144,11 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
 //   * tile t: forward Z1 = X.W1 (2 row blocks x 3 column blocks x 3 K-steps, 3 MFMAs each), act,
 //     head partials over the wave's 48 units (in-lane over the 3 column blocks, then a DPP
 //     reduce-scatter over the 16 lanes of a row group) -> part[t & 1]; split X(t+1); BARRIER;
-//     stage X(t+2); head(t) by EVERY wave for all 32 rows (8 partials summed in fixed wave order:
+//     head(t) by EVERY wave for all 32 rows (8 partials summed in fixed wave order:
 //     the same bits in every wave), dZ2 to the wave's own LDS table; backward: dZ1 in registers
 //     straight from the forward accumulators (lane group g's rows are the K slice 8g .. 8g+7 of
-//     the dW1 GEMM) as the B operand of dW1 += X^T.dZ1, A = X^T from xt.
+//     the dW1 GEMM) as the B operand of dW1 += X^T.dZ1, A = X^T from xt; stage X(t+2) between
+//     the backward rows and the dW1 MFMAs.
 //   Scope: training launches with P >= 32 (at most two images per tile: the configs[3] / Model-96
 //   96x96 step, contiguous or gathered by fit); evaluation, forward and P < 32 launches keep
 //   mlp2_kernel (the branches they need cost this kernel registers it does not have).
@@ -1476,21 +1480,13 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
       }
     }
     VSTAMP(1);
-    // ---- split X(t+1) (own rows, after own pieces landed), then stage X(t+2) into the same raw
-    // rows (only this wave touches them; the split consumed its reads) before the barrier, so the
-    // LDS-DMA issue overlaps the wait; labels rotate over 4 buffers (head(t-1) may still read
-    // buffer t-1 in a slower wave) ----
+    // ---- split X(t+1) (own rows, after own pieces landed); X(t+2) is staged into the same raw
+    // rows after the backward rows below; labels rotate over 4 buffers ----
     if (tile + G < ntiles) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       v_split(xraw, xf + ((it + 1) & 1) * 3 * V_FRAGF, xt + ((it + 1) % 3) * 3 * V_FRAGT, wave);
     }
     VSTAMP(2);
-    if (tile + 2 * G < ntiles) {
-      TileImg t2 = ti;
-      t2.advance(dq, dr);
-      t2.advance(dq, dr);
-      v_stage(args, xraw, lbuf + ((it + 2) & 3) * MLP2_LAB, (int64_t)(tile + 2 * G) * T, t2, wave, lane, Cin);
-    }
     VSTAMP(3);
     bar_lds();
     VSTAMP(4);
@@ -1580,6 +1576,15 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
         dsp[nb] = split_w8(dv * colt[n * 4 + 2]);
       }
       VSTAMP(6);
+      // stage X(t+2) only now: no LDS-DMA is in flight while head / backward rows run their LDS
+      // read-modify-writes (measured: with the DMA in flight across them, 1 - 18 % of launches
+      // lost a dW2 partial)
+      if (tile + 2 * G < ntiles) {
+        TileImg t2 = ti;
+        t2.advance(dq, dr);
+        t2.advance(dq, dr);
+        v_stage(args, xraw, lbuf + ((it + 2) & 3) * MLP2_LAB, (int64_t)(tile + 2 * G) * T, t2, wave, lane, Cin);
+      }
 #pragma unroll
       for (int cb = 0; cb < 6; ++cb) {
         const int off = vt_off(16 * cb + lc, lg);
