@@ -110,7 +110,8 @@ __global__ void __launch_bounds__(SE_NT) seg_mean_kernel(const float* __restrict
 
 // D: key_dim padded to a multiple of 4 (zero lanes past KD, the real key_dim)
 template <int D>
-__global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ in, int ld_in, int C,
+__global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ in, int ld_in, int C, int qoff,
+                                                     const float* __restrict__ ps, int ld_ps,
                                                      float* __restrict__ out, int ld_out, int P, int H,
                                                      int nqb, int KD) {
   __shared__ __attribute__((aligned(16))) float ks[MHA_KB * D];
@@ -127,7 +128,7 @@ __global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ i
   float qv[D], o[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    qv[d] = d < KD ? qrow[C + h * KD + d] : 0.f;
+    qv[d] = d < KD ? qrow[qoff + h * KD + d] : 0.f;
     o[d] = 0.f;
   }
   float m = -INFINITY, l = 0.f;
@@ -136,7 +137,7 @@ __global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ i
     __syncthreads();  // previous block's readers are done
     for (int e = t; e < nk * D; e += MHA_QB) {
       const int j = e / D, d = e - j * D;
-      const float* kr = in + (row0 + k0 + j) * ld_in + C + HD + h * KD;
+      const float* kr = in + (row0 + k0 + j) * ld_in + qoff + HD + h * KD;
       ks[e] = d < KD ? kr[d] : 0.f;
       vs[e] = d < KD ? kr[HD + d] : 0.f;
     }
@@ -193,7 +194,7 @@ __global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ i
   for (int d = 0; d < D; ++d)
     if (d < KD) orow[C + h * KD + d] = o[d] * inv;
   if (h == 0)
-    for (int c = 0; c < C; ++c) orow[c] = qrow[c];
+    for (int c = 0; c < C; ++c) orow[c] = ps[(row0 + qi) * ld_ps + c];
 }
 
 
@@ -215,7 +216,8 @@ __global__ void __launch_bounds__(MHA_QB) mha_kernel(const float* __restrict__ i
 #define MHAM_W 4              // waves per workgroup (32 queries each)
 #define MHAM_KB 128           // keys per LDS block
 template <int D>              // key_dim padded to an even number <= 32
-__global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __restrict__ in, int ld_in, int C,
+__global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __restrict__ in, int ld_in, int C, int qoff,
+                                                               const float* __restrict__ ps, int ld_ps,
                                                                float* __restrict__ out, int ld_out, int P, int H,
                                                                int nqb, int KD) {
   constexpr int DS = D + 1;   // LDS row stride (odd: the 32 key rows of an A read hit distinct banks)
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __re
   // Q^T operand of step t: Q[q][2t + half]
   float qv[D / 2];
   {
-    const float* qr = in + (row0 + (qok ? q : 0)) * ld_in + C + h * KD;
+    const float* qr = in + (row0 + (qok ? q : 0)) * ld_in + qoff + h * KD;
 #pragma unroll
     for (int t = 0; t < D / 2; ++t) {
       const int d = 2 * t + half;
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __re
       const int j = e / D, d = e - j * D;
       float kv = 0.f, vv = 0.f;
       if (j < nk && d < KD) {
-        const float* kr = in + (row0 + k0 + j) * ld_in + C + HD + h * KD;
+        const float* kr = in + (row0 + k0 + j) * ld_in + qoff + HD + h * KD;
         kv = kr[d];
         vv = kr[HD + d];
       }
@@ -308,7 +310,7 @@ __global__ void __launch_bounds__(MHAM_W * 64) mha_mfma_kernel(const float* __re
     const int qa = qb * (MHAM_W * 32), qe = min(qa + MHAM_W * 32, P);
     for (int e = threadIdx.x; e < (qe - qa) * C; e += MHAM_W * 64) {
       const int r = e / C, c = e - r * C;
-      out[(row0 + qa + r) * ld_out + c] = in[(row0 + qa + r) * ld_in + c];
+      out[(row0 + qa + r) * ld_out + c] = ps[(row0 + qa + r) * ld_ps + c];
     }
   }
 }
@@ -337,12 +339,9 @@ extern "C" int hpe_seg_mean(const float* x, float* y, int64_t n_images, int32_t 
   return e == hipSuccess ? HPE_OK : hpe_fail(HPE_ERUNTIME, "hpe_seg_mean: %s", hipGetErrorString(e));
 }
 
-extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, int32_t ld_out,
-                       int64_t n_images, int32_t P, int32_t H, int32_t D, void* stream) {
-  if (!in || !out) return hpe_fail(HPE_EINVAL, "hpe_mha: null argument");
-  if (n_images < 0 || P <= 0 || C < 0 || H <= 0 || D <= 0 || ld_in < C + 3 * H * D || ld_out < C + H * D)
-    return hpe_fail(HPE_EINVAL, "hpe_mha: bad shape P=%d C=%d H=%d D=%d ld_in=%d ld_out=%d", P, C, H, D,
-                    ld_in, ld_out);
+// in rows: q at float offset qoff, then k, v; pass-through rows ps (stride ld_ps) -> out[:, :C]
+static int mha_launch(const float* in, int32_t ld_in, int32_t qoff, const float* ps, int32_t ld_ps, int32_t C,
+                      float* out, int32_t ld_out, int64_t n_images, int32_t P, int32_t H, int32_t D, void* stream) {
   if (n_images == 0) return HPE_OK;
   hipStream_t s = (hipStream_t)stream;
   if (D <= 32 && !getenv("HPE_MHA_VALU")) {
@@ -350,7 +349,7 @@ extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, in
     const int64_t grid = n_images * H * nqb;
     if (grid > 0x7fffffff) return hpe_fail(HPE_EINVAL, "hpe_mha: grid too large");
 #define MHAM_CASE(DD) \
-    case DD: hipLaunchKernelGGL(mha_mfma_kernel<DD>, dim3((unsigned)grid), dim3(MHAM_W * 64), 0, s, in, ld_in, C, out, ld_out, P, H, nqb, D); break;
+    case DD: hipLaunchKernelGGL(mha_mfma_kernel<DD>, dim3((unsigned)grid), dim3(MHAM_W * 64), 0, s, in, ld_in, C, qoff, ps, ld_ps, out, ld_out, P, H, nqb, D); break;
     switch ((D + 1) & ~1) {
       MHAM_CASE(2) MHAM_CASE(4) MHAM_CASE(6) MHAM_CASE(8) MHAM_CASE(10) MHAM_CASE(12) MHAM_CASE(14) MHAM_CASE(16)
       MHAM_CASE(18) MHAM_CASE(20) MHAM_CASE(22) MHAM_CASE(24) MHAM_CASE(26) MHAM_CASE(28) MHAM_CASE(30) MHAM_CASE(32)
@@ -364,7 +363,7 @@ extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, in
   const int64_t grid = n_images * H * nqb;
   if (grid > 0x7fffffff) return hpe_fail(HPE_EINVAL, "hpe_mha: grid too large");
 #define MHA_CASE(DD) \
-  case DD: hipLaunchKernelGGL(mha_kernel<DD>, dim3((unsigned)grid), dim3(MHA_QB), 0, s, in, ld_in, C, out, ld_out, P, H, nqb, D); break;
+  case DD: hipLaunchKernelGGL(mha_kernel<DD>, dim3((unsigned)grid), dim3(MHA_QB), 0, s, in, ld_in, C, qoff, ps, ld_ps, out, ld_out, P, H, nqb, D); break;
   switch ((D + 3) & ~3) {
     MHA_CASE(4)
     MHA_CASE(8)
@@ -379,4 +378,22 @@ extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, in
 #undef MHA_CASE
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? HPE_OK : hpe_fail(HPE_ERUNTIME, "hpe_mha: %s", hipGetErrorString(e));
+}
+
+extern "C" int hpe_mha(const float* in, int32_t ld_in, int32_t C, float* out, int32_t ld_out,
+                       int64_t n_images, int32_t P, int32_t H, int32_t D, void* stream) {
+  if (!in || !out) return hpe_fail(HPE_EINVAL, "hpe_mha: null argument");
+  if (n_images < 0 || P <= 0 || C < 0 || H <= 0 || D <= 0 || ld_in < C + 3 * H * D || ld_out < C + H * D)
+    return hpe_fail(HPE_EINVAL, "hpe_mha: bad shape P=%d C=%d H=%d D=%d ld_in=%d ld_out=%d", P, C, H, D,
+                    ld_in, ld_out);
+  return mha_launch(in, ld_in, C, in, ld_in, C, out, ld_out, n_images, P, H, D, stream);
+}
+
+extern "C" int hpe_mha_xg(const float* qkv, int32_t ld_qkv, const float* xg, int32_t C, float* out, int32_t ld_out,
+                          int64_t n_images, int32_t P, int32_t H, int32_t D, void* stream) {
+  if (!qkv || !out || (C > 0 && !xg)) return hpe_fail(HPE_EINVAL, "hpe_mha_xg: null argument");
+  if (n_images < 0 || P <= 0 || C < 0 || H <= 0 || D <= 0 || ld_qkv < 3 * H * D || ld_out < C + H * D)
+    return hpe_fail(HPE_EINVAL, "hpe_mha_xg: bad shape P=%d C=%d H=%d D=%d ld_qkv=%d ld_out=%d", P, C, H, D,
+                    ld_qkv, ld_out);
+  return mha_launch(qkv, ld_qkv, 0, xg, C, C, out, ld_out, n_images, P, H, D, stream);
 }

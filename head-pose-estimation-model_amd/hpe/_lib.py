@@ -38,6 +38,7 @@ SIGNATURES = {
                                    _vp]),
     'hpe_seg_mean': (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp]),
     'hpe_mha': (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
+    'hpe_mha_xg': (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
     'hpe_last_error': (ctypes.c_char_p, []),
     'hpe_set_exact_fp32': (ctypes.c_int, [ctypes.c_int]),
 }

@@ -6,13 +6,14 @@ every op is row-local and the ordinary row program runs them.  On H x W > 1 maps
 not row-local, so the graph is cut there and run as a staged pipeline, every stage on the GPU:
 
     x --[hpe_se_gate: GAP -> Dense -> Dense -> Multiply, per image]--> xg
-      --[row program B: one Dense producing [xg | q/sqrt(d) | k | v]]--> qkv rows
-      --[hpe_mha: softmax(q k^T) v per image and head, over the H*W tokens]--> [xg | o] rows
+      --[row program B: one Dense producing [q/sqrt(d) | k | v]]--> qkv rows
+      --[hpe_mha_xg: softmax(q k^T) v per image and head, over the H*W tokens; xg copied
+         alongside]--> [xg | o] rows
       --[row program D: attention_output Dense + residual Add + LayerNorm + feed-forward + Add +
          LayerNorm + 1x1-conv regressor, the reference's own layers]--> (yaw, pitch, roll) rows
 
 Programs B and D are ordinary Keras graphs built here from the original layers and weights:
-B's kernel is [I | Wq/sqrt(d) | Wk | Wv]; D reads the [xg | o] row through ONE Dense layer with
+B's kernel is [Wq/sqrt(d) | Wk | Wv]; D reads the [xg | o] row through ONE Dense layer with
 kernel [I; Wo] that stands for the residual Add(xg, attention output) (named like the Add; a
 graph that reads xg or the attention output elsewhere keeps two Dense layers, [I; 0] and [0; Wo]).  The
 Lambda flatten / reshape-back layers are identities on rows.  Forward (predict) only: the
@@ -174,10 +175,10 @@ class SpatialPlan:
             bq, bk, bv = (mw(p, 'bias', (HD,)) for p in ('query', 'key', 'value'))
             wo, bo = mw('attention_output', 'kernel', (HD, C)), mw('attention_output', 'bias', (C,))
             self.mha = dict(H=H, D=D)
-            # program B: [xg | q s | k | v]
-            kb = np.concatenate([np.eye(C, dtype=np.float32), wq * s, wk, wv], axis=1)
-            bb = np.concatenate([np.zeros(C, np.float32), bq * s, bk, bv])
-            self.qkv_config = _model('spatial_qkv', [_input('qkv_in', C), _dense('qkv', C + 3 * HD, ['qkv_in'])],
+            # program B: [q s | k | v] (hpe_mha_xg reads xg from its own rows: no identity block)
+            kb = np.concatenate([wq * s, wk, wv], axis=1)
+            bb = np.concatenate([bq * s, bk, bv])
+            self.qkv_config = _model('spatial_qkv', [_input('qkv_in', C), _dense('qkv', 3 * HD, ['qkv_in'])],
                                      'qkv_in', 'qkv')
             self.qkv_weights = {'qkv/kernel': kb, 'qkv/bias': bb}
             # program D input: [xg | o].  The reference's residual Add(flat, attn) (attention_model.py:
@@ -284,6 +285,6 @@ class SpatialHead:
         H, D = pl.mha['H'], pl.mha['D']
         qkv = self.qkv.forward(xg, P)
         xo = torch.empty((x.shape[0], self.C + H * D), dtype=torch.float32, device=x.device)
-        _lib.check(lib.hpe_mha(_ptr(qkv), qkv.shape[1], self.C, _ptr(xo), xo.shape[1], n, P, H, D, _stream()),
-                   'hpe_mha')
+        _lib.check(lib.hpe_mha_xg(_ptr(qkv), qkv.shape[1], _ptr(xg), self.C, _ptr(xo), xo.shape[1], n, P, H, D,
+                                  _stream()), 'hpe_mha_xg')
         return self.head.forward(xo, P, out=out)

@@ -194,6 +194,12 @@ int hpe_se_gate(const float *x, float *xg, int64_t n_images, int32_t P, int32_t 
 int hpe_seg_mean(const float *x, float *y, int64_t n_images, int32_t P, int32_t C, void *stream);
 int hpe_mha(const float *in, int32_t ld_in, int32_t C, float *out, int32_t ld_out,
             int64_t n_images, int32_t P, int32_t H, int32_t D, void *stream);
+/* hpe_mha_xg: the same attention with the pass-through columns read from their own rows: qkv =
+ * [q H*D (pre-scaled) | k H*D | v H*D] (stride ld_qkv), xg [n_images * P][C] contiguous; out =
+ * [xg | o H*D] (stride ld_out).  The projection that feeds it then computes only q | k | v (no
+ * identity block for xg: 2 * C * C fewer FLOPs and C fewer stored floats per row). */
+int hpe_mha_xg(const float *qkv, int32_t ld_qkv, const float *xg, int32_t C, float *out, int32_t ld_out,
+               int64_t n_images, int32_t P, int32_t H, int32_t D, void *stream);
 
 #ifdef __cplusplus
 }

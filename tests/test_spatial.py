@@ -52,16 +52,16 @@ def _emulate(plan, x, P):
     H, D = plan.mha['H'], plan.mha['D']
     pb = C.compile_graph(plan.qkv_config, plan.qkv_weights, 'fwd', fused=False)
     qkv = EMU.run(pb, _flat(pb, plan.qkv_weights), xg)['out']
-    Cc = plan.C
-    q = qkv[:, Cc:Cc + H * D].reshape(n, P, H, D)
-    k = qkv[:, Cc + H * D:Cc + 2 * H * D].reshape(n, P, H, D)
-    v = qkv[:, Cc + 2 * H * D:].reshape(n, P, H, D)
+    # program B: [q | k | v] rows (hpe_mha_xg takes xg from its own rows)
+    q = qkv[:, :H * D].reshape(n, P, H, D)
+    k = qkv[:, H * D:2 * H * D].reshape(n, P, H, D)
+    v = qkv[:, 2 * H * D:].reshape(n, P, H, D)
     s = np.einsum('bthd,bshd->bhts', q, k)
     a = np.exp(s - s.max(-1, keepdims=True))
     a /= a.sum(-1, keepdims=True)
     o = np.einsum('bhts,bshd->bthd', a, v).reshape(n * P, H * D)
     pd = C.compile_graph(plan.head_config, plan.head_weights, 'fwd', fused=False)
-    return EMU.run(pd, _flat(pd, plan.head_weights), np.concatenate([qkv[:, :Cc], o], axis=1))['out']
+    return EMU.run(pd, _flat(pd, plan.head_weights), np.concatenate([xg, o], axis=1))['out']
 
 
 def _modelC():
@@ -163,3 +163,29 @@ def test_gpu_spatial_large_map_and_p1_consistency():
     sh = SpatialHead(mc, w, torch.device('cuda'))
     staged = sh.forward(torch.from_numpy(x1.reshape(-1, c)).cuda(), 1).cpu().numpy()
     np.testing.assert_allclose(staged, row, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('D,P', [(16, 256), (6, 35), (48, 64)])
+def test_mha_xg_matches_mha(D, P):
+    """hpe_mha_xg (q | k | v rows + the pass-through columns from their own rows) against hpe_mha on
+    the concatenated [xg | q | k | v] rows: identical outputs (same kernels, same arithmetic), for
+    the MFMA core (key_dim <= 32) and the VALU one (key_dim 48)."""
+    import ctypes
+    import torch
+    from hpe import _lib
+    lib = _lib.load()
+    n, C, H = 3, 88, 4
+    g = torch.Generator().manual_seed(D + P)
+    xg = torch.randn((n * P, C), generator=g).cuda()
+    qkv = torch.randn((n * P, 3 * H * D), generator=g).cuda() * 0.5
+    cat = torch.cat([xg, qkv], dim=1).contiguous()
+    o1 = torch.zeros((n * P, C + H * D), device='cuda')
+    o2 = torch.zeros_like(o1)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.hpe_mha(vp(cat), cat.shape[1], C, vp(o1), o1.shape[1], n, P, H, D, st) == 0
+    assert lib.hpe_mha_xg(vp(qkv), qkv.shape[1], vp(xg), C, vp(o2), o2.shape[1], n, P, H, D, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.equal(o2[:, :C], xg)
