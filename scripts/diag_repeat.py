@@ -1,5 +1,6 @@
-"""Run the fused training gradient of sqnu665j at P = 9216 (n images) R times in one process and
-report every run whose result differs from the first (race hunting): prints the differing entries"""
+"""Run the fused training gradient of a checkpoint (default sqnu665j) on side x side maps (default
+96: P = 9216; n images) R times in one process and report every run whose result differs from the
+first (race screen): prints the differing entries.  argv: n R [rid side]"""
 import os
 import sys
 
@@ -14,12 +15,15 @@ from hpe.engine import Engine  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-mc, w = fixture('sqnu665j')
+rid = sys.argv[3] if len(sys.argv) > 3 else 'sqnu665j'
+side = int(sys.argv[4]) if len(sys.argv) > 4 else 96
+mc, w = fixture(rid)
 eng = Engine(mc, w)
-P = 96 * 96
-x = features(n, 96, seed=21, h=96, w=96)
+P = side * side
+c = int(mc['config']['layers'][0]['config']['batch_input_shape'][-1])
+x = features(n, c, seed=21, h=side, w=side)
 y = labels(n, seed=22)
-xt = torch.from_numpy(x.reshape(n * P, 96)).cuda()
+xt = torch.from_numpy(x.reshape(n * P, c)).cuda()
 yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
 gs = [eng.gradient(xt, yt, P, None, n, 1.0 / (n * P * 3), seed=5).cpu().numpy().copy() for _ in range(R)]
 ref = gs[0]
@@ -29,4 +33,4 @@ for i, g in enumerate(gs[1:], 1):
     if len(d):
         nbad += 1
         print('run %d: %d entries differ, first %s' % (i, len(d), d[:12].tolist()), flush=True)
-print('n=%d: %d of %d runs differ from run 0' % (n, nbad, R - 1), flush=True)
+print('%s side %d n=%d: %d of %d runs differ from run 0' % (rid, side, n, nbad, R - 1), flush=True)

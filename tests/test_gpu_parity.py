@@ -336,6 +336,36 @@ def test_train_step_8wave_kernel(F, act, dropout, side, n):
     np.testing.assert_allclose(g_split[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
 
 
+@pytest.mark.parametrize('rid,side,n,R', [('sqnu665j', 96, 2, 40), ('sqnu665j', 96, 24, 12),
+                                          ('stoqa9pt', 88, 8, 24)])
+def test_train_step_bit_repeatable(rid, side, n, R):
+    """Race screen (scripts/diag_repeat.py as a test): the fused training step launched R times on
+    identical inputs gives bit-identical gradients and loss sums.  A missing LDS ordering (a
+    LDS-DMA landing across a read, a partial-sum slot written by two waves) shows up as a rare
+    run that differs in a handful of entries by far less than the tolerance tests allow.
+    sqnu665j at 96x96 runs mlp2v_kernel (n = 2: one or two tiles per workgroup; n = 24: the
+    steady-state X(t+2) staging pipeline), stoqa9pt at 88x88 the 4-wave mlp2_kernel."""
+    from hpe.engine import Engine
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    eng = Engine(mc, w)
+    P = side * side
+    x = features(n, c, seed=21, h=side, w=side)
+    y = labels(n, seed=22)
+    xt = torch.from_numpy(x.reshape(n * P, c)).cuda()
+    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
+    inv = 1.0 / (n * P * 3)
+    ref = eng.gradient(xt, yt, P, None, n, inv, seed=5).cpu().numpy().copy()
+    assert np.isfinite(ref).all()
+    bad = []
+    for r in range(1, R):
+        g = eng.gradient(xt, yt, P, None, n, inv, seed=5).cpu().numpy()
+        d = np.nonzero(g != ref)[0]
+        if len(d):
+            bad.append((r, len(d), d[:8].tolist()))
+    assert not bad, bad
+
+
 def _create_model(F, act, dropout, l2, lr=2.8e-4):
     """train_96.py:65-110 create_model with the given width / activation / rates."""
     keras.backend.clear_session()
