@@ -865,6 +865,56 @@ __global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ w
   if (w == 0 && i < n) grad[i] = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
 }
 
+// one parameter's sum over the workgroup slabs in exactly reduce_kernel's order (wave w's four
+// strided accumulators, then the fixed-order combination of the four wave partials): a fused
+// reduce + optimizer launch gives the bit-identical gradient
+__device__ __forceinline__ float reduce_slabs(const float* __restrict__ p, int grid, int slab) {
+  float part[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int g = w;
+    for (; g + 12 < grid; g += 16) {
+      s0 += p[(size_t)g * slab];
+      s1 += p[(size_t)(g + 4) * slab];
+      s2 += p[(size_t)(g + 8) * slab];
+      s3 += p[(size_t)(g + 12) * slab];
+    }
+    for (; g < grid; g += 4) s0 += p[(size_t)g * slab];
+    part[w] = (s0 + s1) + (s2 + s3);
+  }
+  return (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// Keras legacy optimizer update of parameter i from its gradient g (before gscale / L2)
+__device__ __forceinline__ float optim_update(int kind, float lr, float alpha, float b1, float b2, float eps,
+                                              float gscale, float* __restrict__ w, float* __restrict__ m,
+                                              float* __restrict__ v, float graw, float c2, int64_t i, float& reg) {
+  const float wi = w[i];
+  reg = fmaf(c2 * wi, wi, reg);
+  const float g = fmaf(graw, gscale, 2.f * c2 * wi);
+  float wn;
+  if (kind == HPE_OPT_SGD) {
+    wn = wi - lr * g;
+  } else if (kind == HPE_OPT_ADAM) {
+    float mi = m[i], vi = v[i];
+    mi += (g - mi) * (1.f - b1);
+    vi += (g * g - vi) * (1.f - b2);
+    m[i] = mi;
+    v[i] = vi;
+    wn = wi - (mi * alpha) / (sqrtf(vi) + eps);
+  } else {
+    float mi = m[i], vi = v[i];
+    mi += (g - mi) * (1.f - b1);
+    vi = fmaxf(b2 * vi, fabsf(g));
+    m[i] = mi;
+    v[i] = vi;
+    wn = wi - alpha * (mi / (vi + eps));
+  }
+  w[i] = wn;
+  return wn;
+}
+
 // Keras legacy optimizers (TF ApplyGradientDescent / ApplyAdam / ApplyAdaMax functors)
 __global__ void optim_kernel(int kind, float lr, float alpha, float b1, float b2, float eps,
                              float gscale, float* __restrict__ w, float* __restrict__ wt,
@@ -874,29 +924,7 @@ __global__ void optim_kernel(int kind, float lr, float alpha, float b1, float b2
   float reg = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float wi = w[i];
-    const float c2 = l2[i];
-    reg = fmaf(c2 * wi, wi, reg);
-    const float g = fmaf(grad[i], gscale, 2.f * c2 * wi);
-    float wn;
-    if (kind == HPE_OPT_SGD) {
-      wn = wi - lr * g;
-    } else if (kind == HPE_OPT_ADAM) {
-      float mi = m[i], vi = v[i];
-      mi += (g - mi) * (1.f - b1);
-      vi += (g * g - vi) * (1.f - b2);
-      m[i] = mi;
-      v[i] = vi;
-      wn = wi - (mi * alpha) / (sqrtf(vi) + eps);
-    } else {
-      float mi = m[i], vi = v[i];
-      mi += (g - mi) * (1.f - b1);
-      vi = fmaxf(b2 * vi, fabsf(g));
-      m[i] = mi;
-      v[i] = vi;
-      wn = wi - alpha * (mi / (vi + eps));
-    }
-    w[i] = wn;
+    const float wn = optim_update(kind, lr, alpha, b1, b2, eps, gscale, w, m, v, grad[i], l2[i], i, reg);
     const int tp = tpos[i];
     if (tp >= 0) wt[tp] = wn;
   }
@@ -909,6 +937,37 @@ __global__ void optim_kernel(int kind, float lr, float alpha, float b1, float b2
     regp[0] = grad[n];
     regp[1] = grad[n + 1];
   }
+}
+
+// reduce_kernel + optim_kernel in one launch (single-rank per-step training: no all-reduce between
+// them): each thread sums its parameter over the workgroup slabs in reduce_kernel's order, keeps
+// the flat gradient in grad (same contents as hpe_reduce) and applies the optimizer; block 0 also
+// reduces the 4 loss / aux words.  Only for small persistent grids (the P = 1 per-step path: a few
+// slabs), where the second launch's latency is a sizable part of the step.
+__global__ void __launch_bounds__(256) reduce_optim_kernel(
+    const float* __restrict__ ws, int grid, int slab, int kind, float lr, float alpha, float b1, float b2,
+    float eps, float gscale, float* __restrict__ w, float* __restrict__ wt, float* __restrict__ m,
+    float* __restrict__ v, float* __restrict__ grad, const float* __restrict__ l2, const int* __restrict__ tpos,
+    int64_t n, float* __restrict__ regp) {
+  float reg = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = reduce_slabs(ws + i, grid, slab);
+    grad[i] = gi;
+    const float wn = optim_update(kind, lr, alpha, b1, b2, eps, gscale, w, m, v, gi, l2[i], i, reg);
+    const int tp = tpos[i];
+    if (tp >= 0) wt[tp] = wn;
+  }
+  reg = wave_sum(reg);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = reg;
+  if (blockIdx.x == 0 && threadIdx.x < 4) {
+    const float t = reduce_slabs(ws + n + threadIdx.x, grid, slab);
+    grad[n + threadIdx.x] = t;
+    if (threadIdx.x < 2) regp[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) regp[2 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1269,6 +1328,34 @@ extern "C" int hpe_optim_step(int32_t kind, float lr, float b1, float b2, float 
   const int grid = hpe_optim_grid(n);
   hipLaunchKernelGGL(optim_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, kind, lr,
                      (float)alpha, b1, b2, eps, gscale, w, wt ? wt : w, m, v, grad, l2, tpos, n, regp);
+  HIPCHK(hipGetLastError());
+  return HPE_OK;
+}
+
+extern "C" int hpe_reduce_optim_step(const hpe_program* p, int64_t n_rows, const void* ws, float* grad,
+                                     int32_t kind, float lr, float b1, float b2, float eps, int64_t iter,
+                                     float gscale, float* w, float* wt, float* m, float* v, const float* l2,
+                                     const int32_t* tpos, int64_t n, float* regp, void* stream) {
+  if (!p || !ws || !grad || !w || !l2 || !tpos || !regp) return fail(HPE_EINVAL, "hpe_reduce_optim_step: null argument");
+  if (n != p->hdr[H_NPARAMS_TRAIN])
+    return fail(HPE_EINVAL, "hpe_reduce_optim_step: n = %lld, the program trains %d parameters", (long long)n,
+                p->hdr[H_NPARAMS_TRAIN]);
+  if (kind != HPE_OPT_SGD && (!m || !v)) return fail(HPE_EINVAL, "hpe_reduce_optim_step: Adam/Adamax need m and v");
+  if (iter < 1) return fail(HPE_EINVAL, "hpe_reduce_optim_step: iter must be >= 1");
+  double alpha = lr;
+  if (kind == HPE_OPT_ADAM) {
+    const double b1p = pow((double)b1, (double)iter), b2p = pow((double)b2, (double)iter);
+    alpha = (double)lr * sqrt(1.0 - b2p) / (1.0 - b1p);
+  } else if (kind == HPE_OPT_ADAMAX) {
+    alpha = (double)lr / (1.0 - pow((double)b1, (double)iter));
+  } else if (kind != HPE_OPT_SGD) {
+    return fail(HPE_EINVAL, "hpe_reduce_optim_step: unknown optimizer kind %d", kind);
+  }
+  const int sgrid = hpe_launch_grid(p, n_rows);
+  const int grid = hpe_optim_grid(n);
+  hipLaunchKernelGGL(reduce_optim_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)ws, sgrid,
+                     p->hdr[H_SLAB], kind, lr, (float)alpha, b1, b2, eps, gscale, w, wt ? wt : w, m, v, grad, l2,
+                     tpos, n, regp);
   HIPCHK(hipGetLastError());
   return HPE_OK;
 }

@@ -77,6 +77,7 @@ class Engine:
         self.l2 = torch.from_numpy(base.l2).to(self.device)
         self.tpos = torch.from_numpy(base.tpos).to(self.device)
         self.m = None
+        self._pending = None   # (program, rows, workspace) of a gradient awaiting its fused reduce
         self.v = None
         self._fit_ws = None
         self.iterations = 0
@@ -159,19 +160,30 @@ class Engine:
         _lib.check(lib.hpe_reduce(c.h, n_img * P, _ptr(ws), _ptr(out), _stream()), 'hpe_reduce')
         return out[self.n_train:self.n_train + 2]
 
-    def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0):
-        """fwd + loss + bwd over this rank's images; self.grad = [dL/dparams..., sse, sae, 0, 0]."""
+    # per-step launches whose persistent grid is at most this many workgroups hand the slab
+    # reduction to the optimizer launch (hpe_reduce_optim_step: one launch fewer per step)
+    FUSED_REDUCE_MAX_GRID = 16
+
+    def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0, defer_reduce=False):
+        """fwd + loss + bwd over this rank's images; self.grad = [dL/dparams..., sse, sae, 0, 0].
+        defer_reduce: a single-rank fit step whose next call is optimizer_step may leave the
+        per-workgroup slabs unreduced; optimizer_step then reduces and updates in one launch
+        (self.grad is written by that launch, bit-identical to hpe_reduce's)."""
         if P > 1 and self.spatial() is not None:
             raise ValueError('fit of attention heads runs on 1x1 maps (train_88.py:270-305)')
         c = self.program('train', P)
         lib = _lib.load()
-        ws = c.workspace(n_images * P, self.device)
+        rows = n_images * P
+        ws = c.workspace(rows, self.device)
         _lib.check(lib.hpe_train_step(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), _ptr(y),
                                       n_images, P, _ptr(idx), img_off, float(inv_count),
                                       int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(ws), _stream()),
                    'hpe_train_step')
-        _lib.check(lib.hpe_reduce(c.h, n_images * P, _ptr(ws), _ptr(self.grad), _stream()),
-                   'hpe_reduce')
+        self._pending = None
+        if defer_reduce and lib.hpe_launch_grid(c.h, rows) <= self.FUSED_REDUCE_MAX_GRID:
+            self._pending = (c, rows, ws)
+            return None
+        _lib.check(lib.hpe_reduce(c.h, rows, _ptr(ws), _ptr(self.grad), _stream()), 'hpe_reduce')
         return self.grad
 
     def optimizer_step(self, opt, stats, grad_scale=1.0):
@@ -181,6 +193,18 @@ class Engine:
             self.v = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
         self.iterations += 1
         lib = _lib.load()
+        pend = getattr(self, '_pending', None)
+        if pend is not None:
+            self._pending = None
+            c, rows, ws = pend
+            _lib.check(lib.hpe_reduce_optim_step(c.h, rows, _ptr(ws), _ptr(self.grad), kind,
+                                                 float(opt.learning_rate), float(opt.beta_1),
+                                                 float(opt.beta_2), float(opt.epsilon), self.iterations,
+                                                 float(grad_scale), _ptr(self.params), _ptr(self.params_t),
+                                                 _ptr(self.m), _ptr(self.v), _ptr(self.l2), _ptr(self.tpos),
+                                                 self.n_train, _ptr(stats), _stream()),
+                       'hpe_reduce_optim_step')
+            return
         _lib.check(lib.hpe_optim_step(kind, float(opt.learning_rate), float(opt.beta_1),
                                       float(opt.beta_2), float(opt.epsilon), self.iterations,
                                       float(grad_scale), _ptr(self.params), _ptr(self.params_t),

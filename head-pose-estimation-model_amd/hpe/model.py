@@ -282,7 +282,7 @@ class Model:
                 seed = hrandom.dropout_seed(eng.iterations + 1)
                 if r1 > r0:
                     eng.gradient(xd, yd, P, idx[r0:r1], r1 - r0, 1.0 / (nb * P * 3), seed,
-                                 img_off=r0 - b0)
+                                 img_off=r0 - b0, defer_reduce=world == 1)
                 else:
                     eng.grad.zero_()
                 if world > 1:

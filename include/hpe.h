@@ -94,6 +94,15 @@ int hpe_optim_step(int32_t kind, float lr, float beta_1, float beta_2, float eps
 /* Blocks hpe_optim_step launches (stats holds 2 + this many floats). */
 int hpe_optim_grid(int64_t n);
 
+/* hpe_reduce followed by hpe_optim_step in ONE launch, for a single rank (no all-reduce between
+ * them): grad receives exactly what hpe_reduce writes (bit-identical: same summation order), the
+ * parameters / moments / stats exactly what hpe_optim_step then writes.  n must equal the program's
+ * trained-parameter count.  Used by the per-step fit path at small launch grids (P = 1 batches). */
+int hpe_reduce_optim_step(const hpe_program *prog, int64_t n_rows, const void *workspace, float *grad,
+                          int32_t kind, float lr, float beta_1, float beta_2, float epsilon, int64_t iter,
+                          float grad_scale, float *params, float *params_t, float *m, float *v,
+                          const float *l2, const int32_t *tpos, int64_t n, float *stats, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
  * Keras fit (train_96.py:175-183, train_88.py:355-363) for the reference's own regime: 1x1 maps

@@ -474,3 +474,37 @@ def test_train_88_default_complex_on_biwi_enlarged():
     for k in g.trainable:
         np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
     assert np.isfinite(hist.history['loss']).all()
+
+
+@pytest.mark.parametrize('rid,opt,n', [('sqnu665j', 'adam', 128), ('stoqa9pt', 'sgd', 100),
+                                       ('hrchr82r', 'adamax', 300), ('9w31h50k', 'adam', 77)])
+def test_fused_reduce_optimizer_step_bit_identical(rid, opt, n):
+    """hpe_reduce_optim_step (csrc/hpe_rowprog.hip reduce_optim_kernel: the slab reduction in
+    reduce_kernel's order + the optimizer in one launch, fit's single-rank per-step path) against
+    hpe_reduce + hpe_optim_step: gradient, parameters, moments and stats bit-identical over three
+    steps (mlp2 programs and a generic row program)."""
+    from hpe.engine import Engine
+    from hpe import optimizers as O
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    x = torch.from_numpy(features(n, c, seed=31).reshape(n, c)).cuda()
+    y = torch.from_numpy(labels(n, seed=32).reshape(n, 3).astype(np.float32)).cuda()
+    engs = [Engine(mc, w), Engine(mc, w)]
+    o = O.get({'adam': 'Adam', 'sgd': 'SGD', 'adamax': 'Adamax'}[opt])
+    o.learning_rate = 1e-3
+    ng = engs[0].optim_grid()
+    stats = [torch.zeros(2 + ng, dtype=torch.float32, device='cuda') for _ in engs]
+    for it in range(3):
+        for k, (e, st) in enumerate(zip(engs, stats)):
+            g = e.gradient(x, y, 1, None, n, 1.0 / (n * 3), seed=it + 1, defer_reduce=(k == 1))
+            if k == 1:
+                assert g is None and e._pending is not None, 'small launch expected to defer its reduction'
+            e.optimizer_step(o, st)
+        a, b = engs
+        np.testing.assert_array_equal(a.grad.cpu().numpy(), b.grad.cpu().numpy())
+        np.testing.assert_array_equal(a.params.cpu().numpy(), b.params.cpu().numpy())
+        np.testing.assert_array_equal(a.params_t.cpu().numpy(), b.params_t.cpu().numpy())
+        np.testing.assert_array_equal(stats[0].cpu().numpy(), stats[1].cpu().numpy())
+        if a.m is not None:
+            np.testing.assert_array_equal(a.m.cpu().numpy(), b.m.cpu().numpy())
+            np.testing.assert_array_equal(a.v.cpu().numpy(), b.v.cpu().numpy())
