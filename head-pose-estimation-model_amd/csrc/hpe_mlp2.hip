@@ -1774,23 +1774,6 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
   }
   return launch_k(pick(w), ncb, lds, a, grid, s);
 }
-}  // namespace MLP2_NS
-
-#ifdef MLP2_BIG
-int mlp2_launch_big(const int* w, const Args& a, int grid, hipStream_t s) {
-  return MLP2_NS::launch_pair(w, a, grid, s);
-}
-#else
-using namespace MLP2_NS;
-int mlp2_launch_big(const int* w, const Args& a, int grid, hipStream_t s);
-
-int mlp2_supported(const int* w) {
-  int kh, rbw, ncb, lds, act, drop;
-  geom(w, kh, rbw, ncb, lds, act, drop);
-  const int* o = w + w[H_OPS_OFF];
-  return pick(w) != nullptr && rbw == 1 && ncb >= 1 && ncb <= MLP2_MAXW &&
-         o[O_AUX3] == 3 && (o[O_K] & 3) == 0 && o[O_K] <= 96 && lds <= 160 * 1024;
-}
 
 static int per_cu_of(mlp2_fn k, int ncb, int lds) {
   hipFuncAttributes attr;
@@ -1805,9 +1788,9 @@ static int per_cu_of(mlp2_fn k, int ncb, int lds) {
   return per_cu < 1 ? 1 : per_cu;
 }
 
-// one grid for both instantiations (the exact one recomputes a flagged split launch into the same
-// per-workgroup slabs): the smaller of their occupancies
-int mlp2_grid_cap(const int* w, int n_cu) {
+// resident workgroups per CU of this object's kernels for program w: the smaller of the split and
+// exact instantiations (and of mlp2v_kernel for the training launches that may run it)
+static int cap_per_cu(const int* w) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
   const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds_split(w));
@@ -1816,7 +1799,34 @@ int mlp2_grid_cap(const int* w, int n_cu) {
     const int c = per_cu_of(pick_v<false>(ACT_TANH, ACT_LINEAR), V_NW, v_lds_floats() * 4);
     m = m < c ? m : c;
   }
-  return n_cu * m;
+  return m;
+}
+}  // namespace MLP2_NS
+
+#ifdef MLP2_BIG
+int mlp2_launch_big(const int* w, const Args& a, int grid, hipStream_t s) {
+  return MLP2_NS::launch_pair(w, a, grid, s);
+}
+int mlp2_per_cu_big(const int* w) { return MLP2_NS::cap_per_cu(w); }
+#else
+using namespace MLP2_NS;
+int mlp2_launch_big(const int* w, const Args& a, int grid, hipStream_t s);
+int mlp2_per_cu_big(const int* w);
+
+int mlp2_supported(const int* w) {
+  int kh, rbw, ncb, lds, act, drop;
+  geom(w, kh, rbw, ncb, lds, act, drop);
+  const int* o = w + w[H_OPS_OFF];
+  return pick(w) != nullptr && rbw == 1 && ncb >= 1 && ncb <= MLP2_MAXW &&
+         o[O_AUX3] == 3 && (o[O_K] & 3) == 0 && o[O_K] <= 96 && lds <= 160 * 1024;
+}
+
+// one grid for both instantiations and both objects (the exact one recomputes a flagged split
+// launch into the same per-workgroup slabs; launches of >= MLP2_BIG_ROWS rows run the MLP2_BIG
+// object, whose register counts differ): the smallest of their occupancies
+int mlp2_grid_cap(const int* w, int n_cu) {
+  const int a = MLP2_NS::cap_per_cu(w), b = mlp2_per_cu_big(w);
+  return n_cu * (a < b ? a : b);
 }
 
 int mlp2_launch(const int* w, const Args& a, int grid, hipStream_t s) {
