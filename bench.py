@@ -18,8 +18,13 @@ Also reported (sub-objects of the one JSON line):
   train88    Model-88 create_model on 88x88 maps
   blazeface  configs[4]: unified BlazeFace + both pose heads, batch 1024
   attn       se_transformer_regr_head (attention_model.py:16-72, checkpoint 12uei1sn: SE + 4-head MHA,
-             key_dim 16) on 16x16x88 BlazeFace-tap maps, batch 1024, forward (VALU attention core)
+             key_dim 16) on 16x16x88 BlazeFace-tap maps, batch 1024, forward (exact-fp32 MFMA attention
+             core, mha_mfma_kernel)
   cpu_baseline  the oracle's torch-CPU fp32 restatement of the headline step on a bounded sample
+
+roofline.frac of every line = its algorithmic work per launch / the dominant kernel's own time
+(roofline.dominant_kernel_ms: HIP events the library records around that kernel alone on the launch
+stream, averaged over the timed launches; KernelTimer), so it is derivable from the line itself.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   N > 1 without a torchrun environment: this process starts
@@ -176,10 +181,36 @@ def synth(n_img, seed, device, P=H * W, c=C):
     return x.contiguous(), y.contiguous()
 
 
+class KernelTimer:
+    """HIP events around each launch's dominant kernel only (libhpe.so hpe_kernel_timing: recorded
+    by the library on the launch stream around the fp16-split kernel, not its early-exit exact twin
+    nor the reduce)."""
+
+    def __init__(self, n):
+        from hpe import _lib
+        self.lib, self.n = _lib.load(), n
+
+    def __enter__(self):
+        from hpe import _lib
+        _lib.check(self.lib.hpe_kernel_timing(self.n), 'hpe_kernel_timing')
+        return self
+
+    def __exit__(self, *exc):
+        import ctypes
+        buf = (ctypes.c_float * self.n)()
+        k = self.lib.hpe_kernel_times(buf, self.n)
+        self.lib.hpe_kernel_timing(0)
+        self.ms = [float(v) for v in buf[:max(k, 0)]]
+        return False
+
+    def mean(self):
+        return float(np.mean(self.ms)) if self.ms else float('nan')
+
+
 def run_train(eng, opt, x, y, P, n_local, n_global, rank, world, steps, warmup, dist):
     """Timed training steps (barrier + synchronize on both sides, max over ranks).  Returns
     (seconds, mean ms of the train_step + reduce launches measured with HIP events on the launch
-    stream, mse of the last step)."""
+    stream, mse of the last step, mean ms of the dominant kernel alone (KernelTimer))."""
     inv_count = 1.0 / (n_global * P * 3)
     stats = torch.zeros((steps + warmup + 1, 2 + eng.optim_grid()), device=x.device)
     for i in range(warmup):
@@ -191,30 +222,48 @@ def run_train(eng, opt, x, y, P, n_local, n_global, rank, world, steps, warmup, 
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    kt = KernelTimer(steps)
     t0 = time.perf_counter()
     marks = []
-    for i in range(steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        eng.gradient(x, y, P, None, n_local, inv_count, seed=warmup + i + 1, img_off=rank * n_local)
-        e1.record()
-        marks.append((e0, e1))
+    with kt:
+        for i in range(steps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            eng.gradient(x, y, P, None, n_local, inv_count, seed=warmup + i + 1, img_off=rank * n_local)
+            e1.record()
+            marks.append((e0, e1))
+            if dist is not None:
+                dist.all_reduce(eng.grad)
+            eng.optimizer_step(opt, stats[warmup + i])
+        torch.cuda.synchronize()
         if dist is not None:
-            dist.all_reduce(eng.grad)
-        eng.optimizer_step(opt, stats[warmup + i])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([dt], device=x.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in marks]))
     mse = float(stats[warmup + steps - 1, 0].item()) / (n_global * P * 3)
-    return dt, kms, mse
+    return dt, kms, mse, kt.mean()
+
+
+def train_kernel_name(eng, P):
+    """The kernel libhpe.so runs for a training launch of this program (csrc/hpe_mlp2.hip use_v:
+    mlp2v_kernel for 128 < F <= 384, C_in <= 96 at P >= 32 unless HPE_MLP2_V=0)."""
+    prog = eng.program('train', P).prog
+    if prog.kind == 'res':
+        return 'res_train_kernel'
+    if prog.kind != 'mlp2':
+        return 'rowprog_kernel'
+    if os.environ.get('HPE_EXACT_FP32') == '1':
+        return 'mlp2_kernel (exact fp32)'
+    F_, cin = prog.info['F'], prog.C_in
+    if P >= 32 and 128 < F_ <= 384 and cin <= 96 and os.environ.get('HPE_MLP2_V', '1') != '0':
+        return 'mlp2v_kernel'
+    return 'mlp2_kernel'
 
 
 def _threads_for_cpu(probe):
@@ -469,16 +518,16 @@ def bench_train88(hpe, keras, dev, steps, warmup):
     eng = m._eng()
     n, Pm = PER_GPU, 88 * 88
     x, y = synth(n, 88, dev, P=Pm, c=88)
-    dt, kms, _ = run_train(eng, m.optimizer, x, y, Pm, n, n, 0, 1, steps, warmup, None)
+    dt, kms, _, dom_ms = run_train(eng, m.optimizer, x, y, Pm, n, n, 0, 1, steps, warmup, None)
     flop = 2 * (88 * 64 + 64 * 3) * 2 + 2 * 64 * 3            # fwd + dW + dX(layer 2) per position
-    ach = flop * n * Pm / (kms * 1e-3)
+    ach = flop * n * Pm / (dom_ms * 1e-3)
     return {'workload': 'Model-88 create_model (88-64 softsign-3, dropout 1e-4, l2 1e-6) training, legacy Adam, '
                         '512 images of 88x88 feature maps',
             'value': n * steps / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3 / steps, 'dtype': 'fp32',
-            'kernel': eng.program('train', Pm).prog.kind + '_kernel + reduce_kernel',
+            'kernel': train_kernel_name(eng, Pm),
             'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': gemm_peak()[0] / 1e12, 'unit': 'TFLOP/s',
                          'frac': ach / gemm_peak()[0], 'gemm': gemm_peak()[1], 'traffic': _traffic('train88'),
-                         'kernel_ms': kms, 'flop_per_launch': flop * n * Pm}}
+                         'dominant_kernel_ms': dom_ms, 'step_kernels_ms': kms, 'flop_per_launch': flop * n * Pm}}
 
 
 BLAZE_B = 1024
@@ -607,18 +656,21 @@ def bench_infer(hpe, dev, steps):
         ie.forward(xi, P, out=yo)
     torch.cuda.synchronize()
     es = []
-    t0 = time.perf_counter()
     n_inf = max(10, steps)
-    for _ in range(n_inf):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        ie.forward(xi, P, out=yo)
-        e1.record()
-        es.append((e0, e1))
-    torch.cuda.synchronize()
+    kt = KernelTimer(n_inf)
+    t0 = time.perf_counter()
+    with kt:
+        for _ in range(n_inf):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ie.forward(xi, P, out=yo)
+            e1.record()
+            es.append((e0, e1))
+        torch.cuda.synchronize()
     idt = time.perf_counter() - t0
-    ims = float(np.mean([s.elapsed_time(e) for s, e in es]))
+    fwd_ms = float(np.mean([s.elapsed_time(e) for s, e in es]))
+    ims = kt.mean()
     bytes_launch = INFER_BYTES_POS * INFER_B * P
     return {
         'workload': 'Model-96 hrchr82r head (96-32-16-3, reference weights) forward, batch 256, '
@@ -631,7 +683,7 @@ def bench_infer(hpe, dev, steps):
                      'kernel': {'chain': 'chain_split_kernel (+ guarded chain_fwd_kernel)',
                                 'generic': 'rowprog_kernel'}.get(ie.program('fwd', P).prog.kind, '?')
                      + ' (hpe_forward)',
-                     'kernel_ms': ims, 'bytes_per_launch': bytes_launch,
+                     'dominant_kernel_ms': ims, 'forward_ms': fwd_ms, 'bytes_per_launch': bytes_launch,
                      'flop_per_launch': INFER_FLOP_POS * INFER_B * P}}
 
 
@@ -716,19 +768,23 @@ def main(argv=None):
            'backend': dist.get_backend() if dist is not None else 'none (single process)'}
     if want('train'):
         x, y = synth(PER_GPU, 1234 + rank, dev)
-        dt, train_ms, mse = run_train(eng, m.optimizer, x, y, P, PER_GPU, n_global, rank, world,
-                                      a.steps, a.warmup, dist)
+        dt, train_ms, mse, dom_ms = run_train(eng, m.optimizer, x, y, P, PER_GPU, n_global, rank, world,
+                                              a.steps, a.warmup, dist)
         del x, y
         flop_launch = TRAIN_FLOP_POS * PER_GPU * P
-        achieved = flop_launch / (train_ms * 1e-3)
+        achieved = flop_launch / (dom_ms * 1e-3)
         out.update({
             'value': n_global * a.steps / dt, 'ms_per_step': dt * 1e3 / a.steps,
             'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': gemm_peak()[0] / 1e12,
                          'unit': 'TFLOP/s', 'frac': achieved / gemm_peak()[0], 'gemm': gemm_peak()[1],
                          'traffic': _traffic('train'),
-                         'kernel': {'mlp2': 'mlp2_kernel', 'generic': 'rowprog_kernel'}.get(
-                             eng.program('train', P).prog.kind, '?') + ' + reduce_kernel (hpe_train_step + hpe_reduce)',
-                         'kernel_ms': train_ms, 'flop_per_launch': flop_launch},
+                         'kernel': train_kernel_name(eng, P),
+                         'dominant_kernel_ms': dom_ms,
+                         'frac_from': 'flop_per_launch / dominant_kernel_ms (HIP events around the dominant '
+                                      'kernel alone, every timed step, on the launch stream) / peak',
+                         'step_kernels_ms': train_ms,
+                         'step_kernels': 'hpe_train_step (dominant kernel + exact twin early exit) + hpe_reduce',
+                         'flop_per_launch': flop_launch},
             'train_mse_last_step': mse})
     if want('strong', a.no_strong):
         # configs[3] as written: global batch 4096 split over the ranks (strong scaling)
@@ -736,8 +792,8 @@ def main(argv=None):
         m.set_weights(init_w)
         x, y = synth(n_loc, 4321 + rank, dev)
         st = max(3, a.steps // 4)
-        dt, kms, _ = run_train(eng, m.optimizer, x, y, P, n_loc, n_loc * world, rank, world, st,
-                               min(2, a.warmup), dist)
+        dt, kms, _, _ = run_train(eng, m.optimizer, x, y, P, n_loc, n_loc * world, rank, world, st,
+                                  min(2, a.warmup), dist)
         del x, y
         out['strong'] = {'workload': 'configs[3]: global batch %d images of 96x96 split over %d rank(s) '
                                      '(%d per rank), same model / optimizer' % (n_loc * world, world, n_loc),

@@ -47,16 +47,29 @@ __device__ __forceinline__ float act_grad(int act, float a, float z) {
   }
 }
 
-// SpatialDropout2D keep test: counter hash of (seed, dropout ordinal, image, channel).
-// Restated bit-for-bit by oracle/keras_ref.py:dropout_hash.
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int drop_id, uint64_t image, uint32_t c) {
+// SpatialDropout2D keep test: counter hash of (seed, dropout ordinal, image, channel), restated
+// bit-for-bit by oracle/keras_ref.py:dropout_hash.  One 64-bit splitmix of (seed, ordinal, image) —
+// the same for every channel of an image, so a kernel computing several channels of one image pays
+// it once (the compiler shares it) — then a 32-bit murmur3 finaliser of (base, channel) per channel.
+__device__ __forceinline__ uint32_t drop_base(uint64_t seed, int drop_id, uint64_t image) {
   uint64_t x = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(1 + drop_id);
   x ^= image * 0xBF58476D1CE4E5B9ull;
-  x ^= (uint64_t)c * 0xD6E8FEB86659FD93ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   x ^= x >> 31;
   return (uint32_t)(x >> 32);
+}
+__device__ __forceinline__ uint32_t drop_mix(uint32_t base, uint32_t c) {
+  uint32_t h = base ^ (c * 0x9E3779B9u);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, int drop_id, uint64_t image, uint32_t c) {
+  return drop_mix(drop_base(seed, drop_id, image), c);
 }
 
 struct Epi {
@@ -143,6 +156,10 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// guarded (fp16-split) launches: a ring of guard words per program, indexed by launch epoch; the
+// word HPE_GUARD_RING past a launch's guard word collects which check fired (diagnostics)
+#define HPE_GUARD_RING 16
 
 struct Args {
   const int* prog;
@@ -242,6 +259,11 @@ __device__ __forceinline__ float sum16(const f32x16& a) {
 // hpe_set_exact_fp32(): 1 = exact-fp32 MFMA kernels only (hpe_rowprog.hip)
 bool hpe_exact_fp32();
 
+// hpe_kernel_timing(): HIP events around each program launch's dominant kernel (the fp16-split
+// kernel, not its early-exit exact twin), recorded on the launch stream (hpe_rowprog.hip)
+void hpe_tev_begin(hipStream_t s);
+void hpe_tev_end(hipStream_t s);
+
 // fused 2-layer regressor kernel (hpe_mlp2.hip)
 int mlp2_supported(const int* words);
 int mlp2_grid_cap(const int* words, int n_cu);
@@ -252,6 +274,16 @@ int chain_supported(const int* words);
 int chain_grid_cap(int n_cu);
 int chain_lds_bytes();
 int chain_launch(const int* words_host, const Args& a, int grid, hipStream_t s);
+
+// fused residual-stack training (hpe_res.hip)
+int res_supported(const int* words);
+int res_grid_cap(int n_cu);
+int res_launch(const int* words_host, const Args& a, int grid, hipStream_t s);
+int res_fit_launch(const int* w, const int* dwords, float* params, float* params_t, float* m, float* v,
+                   const float* l2, const int32_t* tpos, const float* x, const float* y_true, const int32_t* perm,
+                   int64_t n, int32_t batch, int32_t kind, float beta_1, float beta_2, float epsilon,
+                   const float* alpha, uint64_t seed_base, int64_t iter0, float* stats, int32_t stats_stride,
+                   void* workspace, hipStream_t s);
 
 // a program's word stream: host copy (kernel geometry) and device copy (kernel argument)
 struct hpe_program;

@@ -797,6 +797,8 @@ static fit_fn fit_pick(const int* w, bool split) {
 extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
   if (!p) return 0;
   const int* w = hpe_prog_words(p);
+  // residual stacks (hpe_res.hip): one workgroup runs the epoch, any batch
+  if (w[H_KIND] == KIND_RES) return w[H_MODE] == MODE_TRAIN && batch >= 1 && res_supported(w) ? 1 : 0;
   if (w[H_KIND] != KIND_MLP2 || w[H_MODE] != MODE_TRAIN) return 0;
   const int* o = w + w[H_OPS_OFF];
   if (o[O_AUX3] != 3 || (o[O_K] & 3) || o[O_K] > 96 || o[O_K] < 4) return 0;
@@ -822,6 +824,7 @@ extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
 extern "C" size_t hpe_fit_workspace_size(const hpe_program* p, int32_t batch) {
   if (!p) return 0;
   const int* w = hpe_prog_words(p);
+  if (w[H_KIND] == KIND_RES) return 64;  // flags only
   const int G = (w[w[H_OPS_OFF] + O_N] + 31) / 32;
   return FIT_PART_OFF * sizeof(int) + (size_t)2 * G * batch * 3 * sizeof(uint64_t);
 }
@@ -838,6 +841,16 @@ extern "C" int hpe_fit_epoch(const hpe_program* p, float* params, float* params_
   if (kind < HPE_OPT_SGD || kind > HPE_OPT_ADAMAX) return hpe_fail(HPE_EINVAL, "hpe_fit_epoch: unknown optimizer %d", kind);
   if (n < 1 || n > (int64_t)1 << 30) return hpe_fail(HPE_EINVAL, "hpe_fit_epoch: bad row count %lld", (long long)n);
   const int* w = hpe_prog_words(p);
+  if (w[H_KIND] == KIND_RES) {
+    if (stats_stride < 3) return hpe_fail(HPE_EINVAL, "hpe_fit_epoch: stats_stride %d < 3", stats_stride);
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(workspace, 0, hpe_fit_workspace_size(p, batch), s) != hipSuccess)
+      return hpe_fail(HPE_ERUNTIME, "hpe_fit_epoch: memset: %s", hipGetErrorString(hipGetLastError()));
+    if (res_fit_launch(w, hpe_prog_dwords(p), params, params_t, m, v, l2, tpos, x, y_true, perm, n, batch, kind,
+                       beta_1, beta_2, epsilon, alpha, seed_base, iter0, stats, stats_stride, workspace, s))
+      return hpe_fail(HPE_ERUNTIME, "hpe_fit_epoch: residual-stack launch failed");
+    return HPE_OK;
+  }
   const int G = (w[w[H_OPS_OFF] + O_N] + 31) / 32;
   if (stats_stride < 2 + 4 * G) return hpe_fail(HPE_EINVAL, "hpe_fit_epoch: stats_stride %d < %d", stats_stride, 2 + 4 * G);
   FitArgs a = {};

@@ -22,7 +22,7 @@ enum {
 };
 
 enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_EVAL = 2 };
-enum { KIND_GENERIC = 0, KIND_MLP2 = 1, KIND_CHAIN = 2 };
+enum { KIND_GENERIC = 0, KIND_MLP2 = 1, KIND_CHAIN = 2, KIND_RES = 3 };
 
 // ---- slot words: LDS float offset, channels, padded channels (even, %8), row stride -----------
 enum { S_OFF = 0, S_C, S_CP, S_STRIDE, S_WORDS = 4 };
@@ -56,8 +56,17 @@ enum {
   // fused narrow chain forward (hpe_chain.hip): x -> dense F1 <= 32 -> [dense F2 <= 32] -> dense 3.
   // Fields: O_K C_in, O_N F1, O_AUX3 F2 (0 = none), O_W W1, O_BIAS b1, O_AUX0 W2, O_AUX1 b2,
   // O_AUX2 W3, O_TBASE b3, O_EACT act1, O_FLAGS act2, O_MODE act3, O_TCOUNT 3.
-  OP_CHAIN = 14
+  OP_CHAIN = 14,
+  // fused residual stack (hpe_res.hip, training): x (C_in 88 | 96) -> dense 16 -> NB x [dense 16 ->
+  // dense 16 -> add(block input) -> act] -> [dense BOT <= 16] -> dense 3 (create_model_complex,
+  // Model-88/attention_model.py:97-169).  Fields: O_K C_in, O_N 16, O_AUX3 NB, O_FLAGS BOT (0 =
+  // none), O_MODE the post-add activation, O_AUX0 word offset of the layer table, O_AUX1 its
+  // entries (dense layers in order: 1 + 2 NB + [1] + 1), RL_WORDS each.
+  OP_RES = 15
 };
+// residual-stack layer table entry: kernel / bias parameter offsets (-1: none), activation,
+// dropout ordinal (-1: none), keep threshold, keep probability (float bits), K, N
+enum { RL_W = 0, RL_B, RL_ACT, RL_DROP, RL_THR, RL_KEEP, RL_K, RL_N, RL_WORDS = 8 };
 
 enum { EW_HAS_B = 1, EW_MUL = 2, EW_AFFINE = 4 };             // OP_EW / OP_EWB flags
 enum { DST_STORE = 0, DST_ACCUM = 1, DST_EPIGRAD = 2 };       // O_MODE of DIN/TDIN/EWB/LNB

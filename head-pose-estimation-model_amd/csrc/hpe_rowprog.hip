@@ -1024,6 +1024,44 @@ bool hpe_exact_fp32() {
   return g_exact == 1;
 }
 
+// ---- dominant-kernel timing (hpe_kernel_timing / hpe_kernel_times) ----
+// a pool of event pairs recorded around each launch's dominant kernel while timing is on; the
+// events are created up front by hpe_kernel_timing, so recording never allocates
+static std::vector<hipEvent_t> g_tev;
+static int g_tev_cap = 0, g_tev_n = 0;
+static bool g_tev_on = false;
+
+void hpe_tev_begin(hipStream_t s) {
+  if (g_tev_on && g_tev_n < g_tev_cap) hipEventRecord(g_tev[2 * g_tev_n], s);
+}
+void hpe_tev_end(hipStream_t s) {
+  if (g_tev_on && g_tev_n < g_tev_cap) hipEventRecord(g_tev[2 * g_tev_n++ + 1], s);
+}
+
+extern "C" int hpe_kernel_timing(int32_t capacity) {
+  g_tev_on = false;
+  g_tev_n = 0;
+  if (capacity <= 0) return HPE_OK;
+  while ((int)g_tev.size() < 2 * capacity) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    g_tev.push_back(e);
+  }
+  g_tev_cap = capacity;
+  g_tev_on = true;
+  return HPE_OK;
+}
+
+extern "C" int hpe_kernel_times(float* ms, int32_t max) {
+  if (!ms && max > 0) return fail(HPE_EINVAL, "hpe_kernel_times: null argument");
+  const int n = g_tev_n < max ? g_tev_n : max;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipEventSynchronize(g_tev[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms[i], g_tev[2 * i], g_tev[2 * i + 1]));
+  }
+  return n;
+}
+
 extern "C" int hpe_set_exact_fp32(int on) {
   const int prev = hpe_exact_fp32() ? 1 : 0;
   g_exact = on ? 1 : 0;
@@ -1031,7 +1069,6 @@ extern "C" int hpe_set_exact_fp32(int on) {
 }
 
 typedef void (*kfn_t)(Args);
-#define HPE_GUARD_RING 16
 
 template <int NW, bool GS>
 static kfn_t pick_acc(int maxacc) {
@@ -1074,6 +1111,7 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
   if (fused && !mlp2_supported(words)) return fail(HPE_EINVAL, "program: unsupported fused 2-layer geometry");
   if (kind == KIND_CHAIN && (!chain_supported(words) || words[H_MODE] != MODE_FWD))
     return fail(HPE_EINVAL, "program: unsupported fused chain geometry");
+  if (kind == KIND_RES && !res_supported(words)) return fail(HPE_EINVAL, "program: unsupported residual-stack geometry");
   const int gs = words[H_GSLOTS];
   if (kind == KIND_GENERIC && !pick_kernel(nw, words[H_MAXACC], gs)) return fail(HPE_EINVAL, "program: no kernel for NW=%d MAXACC=%d GSLOTS=%d", nw, words[H_MAXACC], gs);
   if (gs && kind != KIND_GENERIC) return fail(HPE_EINVAL, "program: global slots are for generic programs only");
@@ -1114,9 +1152,10 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
       nsplit += (int64_t)ncb * nks * 512 + ncb * 32;
     }
   }
-  hipError_t e = hipMalloc(&p->dwords, (n_words + HPE_GUARD_RING) * sizeof(int32_t));
+  // guard ring (HPE_GUARD_RING words) + the matching "which check fired" words (hpe_guard_peek)
+  hipError_t e = hipMalloc(&p->dwords, (n_words + 2 * HPE_GUARD_RING) * sizeof(int32_t));
   if (e != hipSuccess) { delete p; return fail(HPE_ERUNTIME, "hipMalloc: %s", hipGetErrorString(e)); }
-  e = hipMemset(p->dwords + n_words, 0, HPE_GUARD_RING * sizeof(int32_t));
+  e = hipMemset(p->dwords + n_words, 0, 2 * HPE_GUARD_RING * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemcpy(p->dwords, dw.data(), n_words * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e == hipSuccess && nsplit > 0) {
     e = hipMalloc(&p->wsplit, nsplit * sizeof(float));
@@ -1144,6 +1183,8 @@ extern "C" int hpe_program_create(const int32_t* words, int64_t n_words, hpe_pro
     p->grid_cap = mlp2_grid_cap(words, ncu);
   } else if (kind == KIND_CHAIN) {
     p->grid_cap = chain_grid_cap(ncu);
+  } else if (kind == KIND_RES) {
+    p->grid_cap = res_grid_cap(ncu);
   } else {
     kfn_t k = pick_kernel(nw, words[H_MAXACC], gs);
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes_of(words));
@@ -1187,6 +1228,14 @@ extern "C" int hpe_program_destroy(hpe_program* p) {
   return HPE_OK;
 }
 
+extern "C" int hpe_guard_peek(const hpe_program* p, int32_t* out) {
+  if (!p || !out) return fail(HPE_EINVAL, "hpe_guard_peek: null argument");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out + 1, p->dwords + p->n_words, 2 * HPE_GUARD_RING * sizeof(int32_t), hipMemcpyDeviceToHost));
+  out[0] = __atomic_load_n(&p->epoch, __ATOMIC_RELAXED);
+  return HPE_OK;
+}
+
 extern "C" int hpe_launch_grid(const hpe_program* p, int64_t n_rows) {
   if (!p) return 0;
   int64_t ntiles = (n_rows + p->hdr[H_T] - 1) / p->hdr[H_T];
@@ -1220,6 +1269,10 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
     if (chain_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "chain launch: %s", hipGetErrorString(hipGetLastError()));
     return HPE_OK;
   }
+  if (p->hdr[H_KIND] == KIND_RES) {
+    if (res_launch(p->words, a, grid, s)) return fail(HPE_ERUNTIME, "residual-stack launch: %s", hipGetErrorString(hipGetLastError()));
+    return HPE_OK;
+  }
   kfn_t k = pick_kernel(p->hdr[H_NW], p->hdr[H_MAXACC], p->hdr[H_GSLOTS]);
   a.gscr = p->gscr;
   kfn_t ks = p->wsplit && !hpe_exact_fp32() ? pick_split(p->hdr[H_NW], p->hdr[H_MAXACC]) : nullptr;
@@ -1250,19 +1303,23 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
                        (const int*)p->split_tab, a.params, a.params_t, p->wsplit);
     HIPCHK(hipGetLastError());
     a.wsplit = p->wsplit;
+    hpe_tev_begin(s);
     hipLaunchKernelGGL(ks, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
     HIPCHK(hipGetLastError());
+    hpe_tev_end(s);
     hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
     HIPCHK(hipGetLastError());
     return HPE_OK;
   }
   a.guard = nullptr;  // no split launch ahead: the kernel runs unconditionally
   const int npass = p->hdr[H_MODE] == MODE_TRAIN && p->hdr[H_NPASS] > 1 ? p->hdr[H_NPASS] : 1;
+  hpe_tev_begin(s);
   for (int pass = 0; pass < npass; ++pass) {
     a.pass = pass;
     hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
     HIPCHK(hipGetLastError());
   }
+  hpe_tev_end(s);
   return HPE_OK;
 }
 

@@ -2,6 +2,7 @@
 ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950); there is no fallback: every compute
 call goes through these symbols, and a missing library raises at first use."""
 import ctypes
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -42,10 +43,33 @@ SIGNATURES = {
     'hpe_mha': (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
     'hpe_mha_xg': (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
     'hpe_last_error': (ctypes.c_char_p, []),
+    'hpe_build_id': (ctypes.c_char_p, []),
+    'hpe_guard_peek': (ctypes.c_int, [_vp, _vp]),
+    'hpe_kernel_timing': (ctypes.c_int, [_i32]),
+    'hpe_kernel_times': (ctypes.c_int, [_vp, _i32]),
     'hpe_set_exact_fp32': (ctypes.c_int, [ctypes.c_int]),
 }
 
 _lib = None
+_CSRC = os.path.join(os.path.dirname(_HERE), 'csrc')
+_HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'include', 'hpe.h')
+
+
+def source_hash():
+    """The src= field csrc/Makefile stamps into libhpe.so: sha256 of the .hip / .h sources in name
+    order, include/hpe.h and the Makefile (first 16 hex digits); None without the sources."""
+    if not os.path.isdir(_CSRC):
+        return None
+    names = sorted(f for f in os.listdir(_CSRC) if f.endswith('.hip') or f.endswith('.h'))
+    h = hashlib.sha256()
+    for path in [os.path.join(_CSRC, f) for f in names] + [_HEADER, os.path.join(_CSRC, 'Makefile')]:
+        with open(path, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    return load().hpe_build_id().decode()
 
 
 class HPEError(RuntimeError):
@@ -65,6 +89,13 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the library must be built from the sources of this tree (HPE_ALLOW_STALE=1: debug builds)
+    want = source_hash()
+    got = lib.hpe_build_id().decode()
+    if want and 'src=%s ' % want not in got + ' ' and os.environ.get('HPE_ALLOW_STALE') != '1' \
+            and not os.environ.get('HPE_LIB'):
+        raise HPEError('libhpe.so (%s) was built from other sources than this tree (src=%s): '
+                       'rebuild with __graft_entry__.build()' % (got, want))
     _lib = lib
     return lib
 

@@ -31,7 +31,8 @@ S_WORDS = 4
  O_AUX0, O_AUX1, O_AUX2, O_AUX3, O_TBASE, O_TCOUNT, O_F0, O_F1, O_MODE, O_WSEL) = range(24)
 O_WORDS = 24
 (OP_DENSE, OP_TDENSE, OP_EW, OP_LN, OP_LOSS, OP_EPIGRAD, OP_DW, OP_TACC, OP_DIN, OP_TDIN, OP_EWB,
- OP_LNB, OP_MLP2, OP_CHAIN) = range(1, 15)
+ OP_LNB, OP_MLP2, OP_CHAIN, OP_RES) = range(1, 16)
+RL_WORDS = 8           # residual-stack layer table entry (csrc/hpe_prog.h RL_*)
 EW_HAS_B, EW_MUL, EW_AFFINE = 1, 2, 4
 DST_STORE, DST_ACCUM, DST_EPIGRAD = 0, 1, 2
 TACC_GEMM, TACC_BIAS, TACC_DIAG = 0, 1, 2
@@ -369,6 +370,10 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
         mlp2 = _try_mlp2(b, x_t, y_t, modes[mode], n_train, l2c, P)
         if mlp2 is not None:
             return mlp2
+        if mode == 'train':
+            res = _try_res(b, x_t, y_t, n_train, l2c)
+            if res is not None:
+                return res
     prog = _finish(b, x_t, y_t, modes[mode], training, P, T, NW, wg_per_cu, n_train, l2c)
     prog.kind = 'generic'
     return prog
@@ -1036,6 +1041,87 @@ def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
     op[O_FLAGS], op[O_MODE] = rbw, ncb
     return _fused_program(b, op, 1, 32 * rbw, ncb, mode, n_train, l2c, cin,
                           {'kind': 'mlp2', 'F': F, 'waves': ncb})
+
+
+RES_NB = (1, 2, 3, 4)    # residual blocks the fused residual-stack kernel is instantiated for
+RES_CIN = (88, 96)
+
+
+def _try_res(b, x_t, y_t, n_train, l2c):
+    """Recognise train_88.py's default graph, create_model_complex (Model-88/attention_model.py:97-169)
+    and the narrow residual stacks like it: x (88 | 96) -> dense 16 (act, dropout) -> NB x [dense 16
+    (act, dropout) -> dense 16 (act, dropout) -> Add(block input) -> act] -> [dense B <= 16 (act,
+    dropout)] -> dense 3 (act, dropout); emit a KIND_RES training program for csrc/hpe_res.hip."""
+    f = b.fops
+    if len(f) < 5 or any(x.kind not in ('dense', 'ew') for x in f):
+        return None
+    if any(x.kind == 'dense' and (x.transposed or x.w[0] != 'p' or x.act in NEEDS_Z) for x in f):
+        return None
+    if any(x.bias is not None and x.bias[0] != 'p' for x in f if x.kind == 'dense'):
+        return None
+    d0 = f[0]
+    if d0.kind != 'dense' or d0.ins[0] is not x_t or d0.K not in RES_CIN or d0.N != 16:
+        return None
+    i, h, nb, post = 1, d0.out, 0, None
+    while i + 2 < len(f) and f[i].kind == 'dense' and f[i + 2].kind == 'ew':
+        a, c, e = f[i], f[i + 1], f[i + 2]
+        if a.ins[0] is not h or a.K != 16 or a.N != 16 or c.kind != 'dense' or c.ins[0] is not a.out:
+            return None
+        if c.K != 16 or c.N != 16 or len(a.out.consumers) != 1 or len(c.out.consumers) != 1:
+            return None
+        if e.flags != EW_HAS_B or e.f0 != 1.0 or e.f1 != 1.0 or e.drop_id >= 0 or e.act in NEEDS_Z:
+            return None
+        if {id(t) for t in e.ins} != {id(h), id(c.out)} or len(e.ins) != 2:
+            return None
+        if post is not None and e.act != post:
+            return None
+        post = e.act
+        if len(h.consumers) != 2:      # the block's first dense and its Add
+            return None
+        h, i, nb = e.out, i + 3, nb + 1
+    if nb not in RES_NB or len(h.consumers) != 1:
+        return None
+    rest = f[i:]
+    if len(rest) not in (1, 2) or any(x.kind != 'dense' for x in rest):
+        return None
+    if len(rest) == 2:
+        bt, out = rest
+        if bt.ins[0] is not h or bt.K != 16 or not 1 <= bt.N <= 16 or out.ins[0] is not bt.out:
+            return None
+        if len(bt.out.consumers) != 1:
+            return None
+    else:
+        bt, out = None, rest[0]
+        if out.ins[0] is not h:
+            return None
+    if out.out is not y_t or out.N != 3:
+        return None
+
+    def ref(r):
+        return -1 if r is None else r[1]
+    dense = [x for x in f if x.kind == 'dense']
+    table = []
+    for x in dense:
+        ent = [0] * RL_WORDS
+        ent[0], ent[1], ent[2] = ref(x.w), ref(x.bias), x.act
+        ent[3], ent[4], ent[5] = -1, 0, _f2i(1.0)
+        if x.drop_id >= 0:
+            ent[3], ent[4] = x.drop_id, _u2i(dropout_threshold(x.rate))
+            ent[5] = _f2i(np.float32(1.0) - np.float32(x.rate))
+        ent[6], ent[7] = x.K, x.N
+        table += ent
+    op = [0] * O_WORDS
+    op[O_TYPE] = OP_RES
+    op[O_K], op[O_N], op[O_AUX3] = d0.K, 16, nb
+    op[O_FLAGS] = bt.N if bt is not None else 0
+    op[O_MODE] = post
+    op[O_AUX0] = H_WORDS + O_WORDS          # the layer table follows the op words
+    op[O_AUX1] = len(dense)
+    # 512 rows per workgroup: launches of up to 512 rows (every fit batch <= 512) run on ONE
+    # workgroup, in the same order as the whole-epoch kernel (bit-identical paths)
+    return _fused_program(b, op + table, 3, 512, 8, MODE_TRAIN, n_train, l2c, d0.K,
+                          {'kind': 'res', 'blocks': nb, 'bottleneck': bt.N if bt is not None else 0,
+                           'layers': len(dense)})
 
 
 def _fused_program(b, op, kind, T, nw, mode, n_train, l2c, cin, info):

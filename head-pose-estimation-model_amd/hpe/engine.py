@@ -235,11 +235,15 @@ class Engine:
         if getattr(self, '_fit_disabled', False):   # an earlier epoch launch timed out
             return False
         c = self.program('train', 1)
-        return c.prog.kind == 'mlp2' and _lib.load().hpe_fit_supported(c.h, int(batch)) == 1
+        return c.prog.kind in ('mlp2', 'res') and _lib.load().hpe_fit_supported(c.h, int(batch)) == 1
 
     def fit_groups(self):
-        """Workgroups of the whole-epoch launch: one per 32 hidden units."""
-        return -(-int(self.program('train', 1).prog.info['F']) // 32)
+        """Workgroups of the whole-epoch launch: one per 32 hidden units (create_model family); one
+        for the residual stacks (csrc/hpe_res.hip: stats [sse, sae, regularisation loss])."""
+        prog = self.program('train', 1).prog
+        if prog.kind == 'res':
+            return 1
+        return -(-int(prog.info['F']) // 32)
 
     def _alphas(self, opt, steps):
         """Per-iteration optimizer step sizes, computed exactly as hpe_optim_step does (double

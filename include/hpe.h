@@ -179,6 +179,25 @@ int hpe_gather_features(const int32_t *count, const int32_t *det_index, int64_t 
 
 const char *hpe_last_error(void);
 
+/* Build stamp: "src=<sha256/16 of the library's sources> git=<commit>[-dirty]" (csrc/Makefile).  The
+ * Python binding recomputes the source hash from the tree it runs in and refuses a library built
+ * from other sources, so a run's kernels are provably the checkout's. */
+const char *hpe_build_id(void);
+
+/* Dominant-kernel timing (bench.py's roofline): hpe_kernel_timing(capacity) turns timing on for
+ * the next `capacity` program launches (0 turns it off): hpe_forward / hpe_train_step record a HIP
+ * event pair on their stream around the launch's dominant kernel only (the fp16-split kernel, not
+ * its early-exit exact twin, nor hpe_reduce).  hpe_kernel_times waits for the recorded pairs and
+ * writes their elapsed milliseconds to ms[0 .. n); returns n (<= max). */
+int hpe_kernel_timing(int32_t capacity);
+int hpe_kernel_times(float *ms, int32_t max);
+
+/* Diagnostics (race screens; synchronises the device, so not for the hot path): out[0] = the
+ * program's last launch epoch, out[1 .. 16] its guard ring (word e % 16 holds e when launch e's
+ * fp16-split kernel flagged a non-finite value and its exact-fp32 twin recomputed the step),
+ * out[17 .. 32] which check fired per ring slot (mlp2v_kernel: 1 forward sums, 2 dW1 flush). */
+int hpe_guard_peek(const hpe_program *prog, int32_t *out);
+
 /* Precision of the regressor GEMMs (process-wide; returns the previous setting).  Default 0: the
  * fused kernels run their fp32 GEMMs as three fp16 MFMAs per product (hi/lo split, fp32
  * accumulate, ~2^-22 relative per product; csrc/hpe_common.h mfma3), and a launch whose split

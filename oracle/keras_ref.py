@@ -62,14 +62,23 @@ def _mix64(z):
 
 
 def dropout_hash(seed, drop_id, image, chan):
-    """uint32 hash of (seed, dropout-layer ordinal, image index in batch, channel)."""
+    """uint32 hash of (seed, dropout-layer ordinal, image index in batch, channel): a 64-bit
+    splitmix of (seed, ordinal, image), then a 32-bit murmur3 finaliser of (its high word, channel)
+    (csrc/hpe_common.h drop_base / drop_mix)."""
     with np.errstate(over='ignore'):
         image = np.asarray(image, dtype=np.uint64)
         chan = np.asarray(chan, dtype=np.uint64)
         x = np.uint64((int(seed) + 0x9E3779B97F4A7C15 * (1 + int(drop_id))) & M64)
         x = x ^ (image * np.uint64(0xBF58476D1CE4E5B9))
-        x = x ^ (chan * np.uint64(0xD6E8FEB86659FD93))
-        return (_mix64(x) >> np.uint64(32)).astype(np.uint32)
+        base = (_mix64(x) >> np.uint64(32)).astype(np.uint64)
+        m32 = np.uint64(0xFFFFFFFF)
+        h = base ^ ((chan * np.uint64(0x9E3779B9)) & m32)
+        h = h ^ (h >> np.uint64(16))
+        h = (h * np.uint64(0x85EBCA6B)) & m32
+        h = h ^ (h >> np.uint64(13))
+        h = (h * np.uint64(0xC2B2AE35)) & m32
+        h = h ^ (h >> np.uint64(16))
+        return h.astype(np.uint32)
 
 
 def dropout_threshold(rate):

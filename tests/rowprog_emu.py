@@ -65,14 +65,22 @@ def _dact(a, v, z):
 
 
 def _hash(seed, did, img, ch):
+    """csrc/hpe_common.h drop_hash: 64-bit splitmix of (seed, ordinal, image), 32-bit finaliser of
+    (its high word, channel)."""
     with np.errstate(over='ignore'):
         x = np.uint64((int(seed) + 0x9E3779B97F4A7C15 * (1 + int(did))) & ((1 << 64) - 1))
         x = x ^ (img.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9))
-        x = x ^ (ch.astype(np.uint64) * np.uint64(0xD6E8FEB86659FD93))
         x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         x = x ^ (x >> np.uint64(31))
-        return (x >> np.uint64(32)).astype(np.uint32)
+        b = (x >> np.uint64(32)).astype(np.uint32)
+        h = b ^ (ch.astype(np.uint32) * np.uint32(0x9E3779B9))
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x85EBCA6B)
+        h = h ^ (h >> np.uint32(13))
+        h = h * np.uint32(0xC2B2AE35)
+        h = h ^ (h >> np.uint32(16))
+        return h.astype(np.uint32)
 
 
 def run(prog, params, x_rows, P=1, y_img=None, inv_count=1.0, seed=0, img_off=0):

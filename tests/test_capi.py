@@ -35,3 +35,13 @@ def test_error_path_without_gpu():
     rc = lib.hpe_program_create(None, 0, ctypes.byref(h))
     assert rc == 1
     assert b'null' in lib.hpe_last_error()
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason='libhpe.so not built')
+def test_build_stamp_matches_tree_sources():
+    """libhpe.so carries the hash of the sources it was built from
+    (csrc/Makefile hpe_build.o) and the binding refuses a library built from other sources, so the
+    kernels a run loads are this checkout's."""
+    bid = _lib.build_id()
+    assert bid.startswith('src=') and ' git=' in bid
+    assert bid.split()[0] == 'src=' + _lib.source_hash()

@@ -73,6 +73,17 @@ def test_unified_model_embeds_selected_heads():
         assert np.array_equal(u['model_10/' + k], v)
 
 
+def test_dropout_hash_restatements_agree():
+    """The emulator's copy of the kernels' dropout hash (tests/rowprog_emu.py) equals the oracle's,
+    over seeds, ordinals, images past 2^32 and channels."""
+    import rowprog_emu as E
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 1 << 40, 5000, dtype=np.uint64)
+    ch = rng.integers(0, 1024, 5000, dtype=np.uint64)
+    for seed, did in ((0, 0), (123456789, 3), ((1 << 64) - 5, 17)):
+        np.testing.assert_array_equal(E._hash(seed, did, img, ch), K.dropout_hash(seed, did, img, ch))
+
+
 def test_dropout_hash_rate():
     m = K.dropout_mask(123, 0, 4096, 64, 0.3)
     keep = (m > 0).mean()
