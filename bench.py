@@ -255,7 +255,7 @@ def train_kernel_name(eng, P):
     mlp2v_kernel for 128 < F <= 384, C_in <= 96 at P >= 32 unless HPE_MLP2_V=0)."""
     prog = eng.program('train', P).prog
     if prog.kind == 'res':
-        return 'res_train_kernel'
+        return 'wide_train_kernel' if prog.info.get('blocks') == 0 else 'res_train_kernel'
     if prog.kind != 'mlp2':
         return 'rowprog_kernel'
     if os.environ.get('HPE_EXACT_FP32') == '1':

@@ -669,6 +669,213 @@ __global__ void __launch_bounds__(256) bf_direct_kernel(BfArgs a) {
   }
 }
 
+
+// one op of a stage (host-filled from its BFO record)
+struct BfSub {
+  int s, h, w, ho, wo, cin, cinp, cout, coutp, ks, nct, nc, res, relu, dw, padt, padl, dww, pww, pwb;
+  int gsrc;     // 1: the source map is the stage input in global memory (first op), 0: the LDS map
+  int lds_out;  // 1: the output map stays in LDS (blocks)
+  int gdst, gdst2, split, ostride;  // global output buffer(s): taps (gdst), heads (split epilogue); -1 none
+};
+#define BFS_MAX 16
+struct BfStageArgs {
+  BfSub op[BFS_MAX];
+  int nops, cs, map_floats, wt_floats;
+  const float* params;
+  const float* src;
+  float* bufs[BF_NBUF];
+};
+
+// ------------------------------------------------------------------------------------------------
+// stage: the small-map tail of the backbone (every block from the first one whose output map has
+// <= 256 positions, e.g. 32x32 -> 16x16 s2 onwards) and the detector heads, ONE workgroup per image,
+// the activation map resident in LDS across all its layers.  The per-op kernels above read and
+// write every intermediate map through HBM (16x16 and 8x8 maps: 0.12-0.24 of HBM bandwidth, each
+// op's launch too short to fill the chip); here the only HBM traffic is the stage's input map,
+// the two taps and the head outputs.
+//   LDS: map [HW][CS] (in place: a block's outputs stay in registers until every wave has read
+//        its inputs, one barrier, then overwrite them; a stride-2 block's smaller output overlays
+//        the start of its input the same way) | W^T of the current op (fp16 hi/lo pairs) | dw table
+//   per op: <= 8 wave tasks (32-position chunk x group of NC output-channel chunks of 32), the same
+//        arithmetic as bf_block_kernel / bf_direct_kernel (depthwise bias + 9 taps in order, fp16-
+//        split MFMA over ascending channel quads, bias, residual, ReLU), so the outputs are
+//        bit-identical to the per-op path; the next op's weights are loaded into registers while
+//        this op computes and written to LDS after its barrier (two barriers per op).
+// ------------------------------------------------------------------------------------------------
+#define BFS_NW 8
+#define BFS_PF 6     // float4 of the next op's W^T + dw table per thread (checked on the host)
+
+__device__ __forceinline__ void bfs_wload(const BfSub& o, const float* P_, f32x4 (&pf)[BFS_PF]) {
+  const int kq = o.cinp >> 2, nW = o.coutp * kq, nT = nW + (o.dw ? 10 * kq : 0);
+#pragma unroll
+  for (int i = 0; i < BFS_PF; ++i) {
+    const int e = threadIdx.x + i * (BFS_NW * 64);
+    const int n = e / kq, q = e - n * kq;
+    const int off = e < nW ? o.pww + n * o.cinp + 4 * q : (e < nT ? o.dww + 4 * (e - nW) : 0);
+    pf[i] = ld4(P_ + off);
+  }
+}
+
+__device__ __forceinline__ void bfs_wstore(const BfSub& o, const f32x4 (&pf)[BFS_PF], float* wt, float* dwt) {
+  const int kq = o.cinp >> 2, nW = o.coutp * kq, nT = nW + (o.dw ? 10 * kq : 0);
+#pragma unroll
+  for (int i = 0; i < BFS_PF; ++i) {
+    const int e = threadIdx.x + i * (BFS_NW * 64);
+    const int n = e / kq, q = e - n * kq;
+    if (e < nW) *(f32x4*)(wt + n * o.ks + 4 * q) = split_w(pf[i]);
+    else if (e < nT) *(f32x4*)(dwt + 4 * (e - nW)) = pf[i];
+  }
+}
+
+// one wave task of op o: acc[j] (j < o.nc) = the final outputs (bias, residual, ReLU applied) of
+// output-channel chunk grp * nc + j at the 32 positions of chunk `chunk`; src = the input map
+// (global: the stage input of this image, channel stride cinp; LDS: the resident map, stride cs)
+#define BFS_MAXNC 3  // output-channel chunks per wave task (acc registers: 16 each)
+template <bool G, bool DW, int RES>
+__device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int ss, const float* wt,
+                                         const float* dwt, const float* P_, int chunk, int grp,
+                                         f32x16 (&acc)[BFS_MAXNC]) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int lgWo = __builtin_ctz(o.wo);
+  const int p = chunk * 32 + l32;
+  const int oy = p >> lgWo, ox = p & (o.wo - 1);
+  int toff[9];
+  uint32_t tmask = 0;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp) {
+    const int iy = oy * o.s - o.padt + tp / 3, ix = ox * o.s - o.padl + tp % 3;
+    const bool ok = iy >= 0 && iy < o.h && ix >= 0 && ix < o.w;
+    toff[tp] = ok ? (iy * o.w + ix) * ss : 0;
+    tmask |= ok ? (1u << tp) : 0u;
+  }
+  const int cen = (oy * o.w + ox) * ss;
+#pragma unroll
+  for (int j = 0; j < BFS_MAXNC; ++j) acc[j] = (f32x16){};
+  const int n0 = grp * o.nc * 32 + l32;
+#pragma unroll 2
+  for (int c0 = 4 * half; c0 < o.cinp; c0 += 8) {
+    f32x4 av;
+    if (DW) {
+      f32x4 xv[9];
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(src + toff[tp] + c0);
+      av = ld4(dwt + 9 * o.cinp + c0);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const f32x4 x = (tmask >> tp) & 1u ? xv[tp] : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 wv = ld4(dwt + tp * o.cinp + c0);
+        av.x = fmaf(x.x, wv.x, av.x);
+        av.y = fmaf(x.y, wv.y, av.y);
+        av.z = fmaf(x.z, wv.z, av.z);
+        av.w = fmaf(x.w, wv.w, av.w);
+      }
+    } else {
+      av = ld4(src + cen + c0);
+    }
+#pragma unroll
+    for (int j = 0; j < BFS_MAXNC; ++j) {
+      if (j < o.nc) {
+        const int n = n0 + 32 * j;
+        const f32x4 wv = n < o.coutp ? ld4(wt + n * o.ks + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[j] = mfma_split(av, wv, acc[j]);
+      }
+    }
+  }
+  // epilogue values: lane = output channel n, registers = 16 positions of the chunk
+#pragma unroll
+  for (int j = 0; j < BFS_MAXNC; ++j) {
+    if (j >= o.nc) continue;
+    const int n = n0 + 32 * j;
+    const float bias = n < o.coutp ? P_[o.pwb + n] : 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+      const int qy = q >> lgWo, qx = q & (o.wo - 1);
+      float v = acc[j][g] + bias;
+      if (RES == BF_RES_ID) {
+        if (n < o.cinp) v += src[(qy * o.w + qx) * ss + n];
+      } else if (RES == BF_RES_MAXPOOL) {
+        if (n < o.cinp) {
+          const float* t = src + ((2 * qy) * o.w + 2 * qx) * ss + n;
+          v += fmaxf(fmaxf(t[0], t[ss]), fmaxf(t[o.w * ss], t[o.w * ss + ss]));
+        }
+      }
+      if (DW && o.relu) v = v > 0.f ? v : 0.f;
+      acc[j][g] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BFS_NW * 64) bf_stage_kernel(BfStageArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* map = lds;
+  float* wt = lds + a.map_floats;
+  float* dwt = wt + a.wt_floats;
+  const int64_t img = blockIdx.x;
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const float* P_ = a.params;
+  const int cs = a.cs;
+  f32x4 pf[BFS_PF];
+  bfs_wload(a.op[0], P_, pf);
+  bfs_wstore(a.op[0], pf, wt, dwt);
+  __syncthreads();
+  for (int i = 0; i < a.nops; ++i) {
+    const BfSub& o = a.op[i];
+    if (i + 1 < a.nops) bfs_wload(a.op[i + 1], P_, pf);
+    const int ngrp = o.nct / o.nc;
+    const int ntask = ((o.ho * o.wo) >> 5) * ngrp;
+    const int chunk = wave / ngrp, grp = wave - chunk * ngrp;
+    f32x16 acc[BFS_MAXNC];
+    if (wave < ntask) {
+      const float* gs = a.src + img * o.h * o.w * o.cinp;
+      if (o.gsrc) {
+        if (o.res == BF_RES_MAXPOOL) bfs_task<true, true, BF_RES_MAXPOOL>(o, gs, o.cinp, wt, dwt, P_, chunk, grp, acc);
+        else bfs_task<true, true, BF_RES_ID>(o, gs, o.cinp, wt, dwt, P_, chunk, grp, acc);
+      } else if (!o.dw) {
+        bfs_task<false, false, BF_RES_NONE>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+      } else if (o.res == BF_RES_MAXPOOL) {
+        bfs_task<false, true, BF_RES_MAXPOOL>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+      } else {
+        bfs_task<false, true, BF_RES_ID>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+      }
+    }
+    __syncthreads();  // every wave's reads of the map and of W^T are done
+    if (wave < ntask) {
+      const int64_t hwo = o.ho * o.wo;
+      float* gd = o.gdst >= 0 ? a.bufs[o.gdst] : nullptr;
+      float* gd2 = o.split ? a.bufs[o.gdst2] : nullptr;
+#pragma unroll
+      for (int j = 0; j < BFS_MAXNC; ++j) {
+        if (j >= o.nc) continue;
+        const int n = (grp * o.nc + j) * 32 + l32;
+        if (n >= o.coutp) continue;
+        if (o.lds_out) {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) map[(chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * cs + n] = acc[j][g];
+        }
+        if (!gd) continue;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+          const float v = acc[j][g];
+          {
+            const int64_t pos = img * hwo + q;
+            if (o.split) {
+              if (n < o.split) gd[pos * o.split + n] = v;
+              else if (n < o.cout) gd2[pos * (o.cout - o.split) + (n - o.split)] = v;
+            } else if (n < o.ostride) {
+              gd[pos * o.ostride + n] = v;
+            }
+          }
+        }
+      }
+    }
+    if (i + 1 < a.nops) bfs_wstore(a.op[i + 1], pf, wt, dwt);
+    __syncthreads();  // outputs and the next op's weights visible
+  }
+}
+
 typedef void (*bf_fn)(BfArgs);
 
 // compile-time channel specialisations of the BlazeFace 64x64 / 32x32 stages (CS = KS = CINP + 4,
@@ -734,8 +941,56 @@ struct hpe_blazeface {
   int n_cu;
 };
 
-static int check_op(const int* f, int i) {
+// stage task split: the fewest output-channel chunks per wave task (most waves busy) that keeps
+// every task of an op on its own wave (<= BFS_NW tasks: results stay in registers over the barrier)
+static int bfs_nc(int nchunk, int nct) {
+  for (int nc = 1; nc <= nct && nc <= BFS_MAXNC; ++nc)
+    if (nct % nc == 0 && nchunk * (nct / nc) <= BFS_NW) return nc;
+  return 0;
+}
+
+static int check_stage(const int* f, int i, int rest) {
+  const int ni = f[BFO_NI], cs = f[BFO_CS], mapf = f[BFO_ROWS], wtf = f[BFO_COLS], lds = f[BFO_LDS];
+  if (ni < 1 || ni > BFS_MAX || ni > rest) return hpe_fail(HPE_EINVAL, "blazeface stage %d: %d ops (max %d, %d follow)", i, ni, BFS_MAX, rest);
+  if (cs < 8 || cs % 4 || mapf < 0 || mapf % 4 || wtf < 0 || wtf % 4 || lds > 160 * 1024 || lds < 4 * (mapf + wtf))
+    return hpe_fail(HPE_EINVAL, "blazeface stage %d: LDS geometry", i);
+  const int dwf = lds / 4 - mapf - wtf;
+  int last_dst = -1;
+  for (int k = 0; k < ni; ++k) {
+    const int* g = f + (k + 1) * BFO_WORDS;
+    const int kind = g[BFO_KIND], dw = g[BFO_DW], s = g[BFO_STRIDE];
+    const int ho = g[BFO_HO], wo = g[BFO_WO], h = g[BFO_H], w = g[BFO_W], cinp = g[BFO_CINP], coutp = g[BFO_COUTP];
+    if (kind != BF_BLOCK && kind != BF_DIRECT) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: kind %d", i, k, kind);
+    if (wo <= 0 || (wo & (wo - 1)) || (ho * wo) % 32 || ho * wo > 32 * BFS_NW || g[BFO_NCT] > 4 ||
+        !bfs_nc((ho * wo) >> 5, g[BFO_NCT]))
+      return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: map / channel-chunk geometry", i, k);
+    if ((coutp + (dw ? 10 : 0)) * (cinp / 4) > BFS_PF * BFS_NW * 64 || coutp * g[BFO_KS] > wtf || (dw && 10 * cinp > dwf))
+      return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: weights exceed the stage's share", i, k);
+    if (dw ? (g[BFO_RES] != BF_RES_ID && g[BFO_RES] != BF_RES_MAXPOOL) || !g[BFO_RELU] : g[BFO_RELU])
+      return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: residual / ReLU variant", i, k);
+    if ((g[BFO_RES] == BF_RES_MAXPOOL && (s != 2 || h != 2 * ho || w != 2 * wo || g[BFO_PADT] || g[BFO_PADL])) ||
+        (g[BFO_RES] == BF_RES_ID && (s != 1 || h != ho || w != wo)))
+      return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: stride / residual geometry", i, k);
+    if (k == 0) {
+      if (!dw || g[BFO_SRC] == BF_BUF_IMG) return hpe_fail(HPE_EINVAL, "blazeface stage %d: must start with a block reading a map", i);
+    } else {
+      if (g[BFO_SRC] != last_dst || h * w * cs > mapf || cinp > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: source is not the resident map", i, k);
+      if (!dw && last_dst < BF_BUF_OUT0) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: heads must read a tap", i, k);
+    }
+    if (dw) {
+      if (ho * wo * cs > mapf || coutp > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: output map exceeds LDS", i, k);
+      if (g[BFO_SPLIT] || g[BFO_OSTRIDE] != coutp) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: block output stride", i, k);
+      last_dst = g[BFO_DST];
+    } else if (g[BFO_RES] != BF_RES_NONE || g[BFO_DST] < BF_BUF_OUT0) {
+      return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: heads geometry", i, k);
+    }
+  }
+  return 0;
+}
+
+static int check_op(const int* f, int i, int rest) {
   const int kind = f[BFO_KIND];
+  if (kind == BF_STAGE) return check_stage(f, i, rest);
   if (kind != BF_STEM && kind != BF_BLOCK && kind != BF_ROWS && kind != BF_DIRECT) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
   if (kind == BF_DIRECT) {
     const int s = f[BFO_STRIDE], dw = f[BFO_DW], wo = f[BFO_WO], ho = f[BFO_HO];
@@ -826,7 +1081,7 @@ extern "C" int hpe_blazeface_create(const int32_t* words, int64_t n_words, hpe_b
   const int nops = words[BFH_NOPS], off = words[BFH_OPS_OFF];
   if (nops <= 0 || off < BFH_WORDS || off + (int64_t)nops * BFO_WORDS > n_words) return hpe_fail(HPE_EINVAL, "blazeface: bad op table");
   for (int i = 0; i < nops; ++i) {
-    const int rc = check_op(words + off + i * BFO_WORDS, i);
+    const int rc = check_op(words + off + i * BFO_WORDS, i, nops - 1 - i);
     if (rc) return rc;
   }
   hpe_blazeface* h = (hpe_blazeface*)calloc(1, sizeof(hpe_blazeface));
@@ -872,6 +1127,40 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
   const int* ops = h->words + h->words[BFH_OPS_OFF];
   for (int i = 0; i < h->nops; ++i) {
     const int* f = ops + i * BFO_WORDS;
+    if (f[BFO_KIND] == BF_STAGE) {  // the next BFO_NI records as one launch, one workgroup per image
+      if (n_images > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
+      BfStageArgs sa;
+      memset(&sa, 0, sizeof sa);
+      const int ni = f[BFO_NI];
+      sa.nops = ni;
+      sa.cs = f[BFO_CS];
+      sa.map_floats = f[BFO_ROWS];
+      sa.wt_floats = f[BFO_COLS];
+      sa.params = params;
+      for (int b = 0; b < BF_NBUF; ++b) sa.bufs[b] = bufs[b];
+      for (int k = 0; k < ni; ++k) {
+        const int* g = f + (k + 1) * BFO_WORDS;
+        BfSub& o = sa.op[k];
+        o.s = g[BFO_STRIDE]; o.h = g[BFO_H]; o.w = g[BFO_W]; o.ho = g[BFO_HO]; o.wo = g[BFO_WO];
+        o.cin = g[BFO_CIN]; o.cinp = g[BFO_CINP]; o.cout = g[BFO_COUT]; o.coutp = g[BFO_COUTP];
+        o.ks = g[BFO_KS]; o.nct = g[BFO_NCT]; o.nc = bfs_nc((o.ho * o.wo) >> 5, o.nct);
+        o.res = g[BFO_RES]; o.relu = g[BFO_RELU]; o.dw = g[BFO_DW]; o.padt = g[BFO_PADT]; o.padl = g[BFO_PADL];
+        o.dww = g[BFO_DWW]; o.pww = g[BFO_PWW]; o.pwb = g[BFO_PWB];
+        o.gsrc = k == 0;
+        if (k == 0) sa.src = bufs[g[BFO_SRC]];
+        o.lds_out = g[BFO_DW] ? 1 : 0;
+        o.gdst = g[BFO_DW] ? (g[BFO_DST] >= BF_BUF_OUT0 ? g[BFO_DST] : -1) : g[BFO_DST];
+        o.split = g[BFO_SPLIT];
+        o.gdst2 = o.split ? g[BFO_DST2] : -1;
+        o.ostride = g[BFO_OSTRIDE];
+      }
+      hipFuncSetAttribute((const void*)bf_stage_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, f[BFO_LDS]);
+      hipLaunchKernelGGL(bf_stage_kernel, dim3((unsigned)n_images), dim3(BFS_NW * 64), f[BFO_LDS], s, sa);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hpe_fail(HPE_ERUNTIME, "blazeface stage %d launch: %s", i, hipGetErrorString(e));
+      i += ni;
+      continue;
+    }
     BfArgs a;
     memcpy(a.f, f, sizeof a.f);
     a.params = params;

@@ -180,7 +180,12 @@ struct Args {
   float* gscr;       // rowprog_kernel<..., GS = true>: per-workgroup slot scratch (H_GSLOTS programs)
   int pass;          // rowprog_kernel: dW-block pass of a multi-pass (H_NPASS) training program
   const float* wsplit;  // rowprog_kernel<..., SPLIT = true>: pre-split OP_DENSE weights (O_AUX3 offsets)
+  float x_bound;        // caller's bound on max |x| (0: unknown); < the split's data range: no exact twin
 };
+
+// the fp16 split's data-side range (|d| < 65504 / 2^SPLIT_SHIFT): a launch whose inputs are known to
+// lie below it cannot overflow on the data side (the weight / dZ sides are power-of-two scaled)
+#define SPLIT_DATA_RANGE 64.f
 
 // ------------------------------------------------------------------------------------------------
 // fp32 GEMMs on fp16 MFMA at fp32 accuracy ("3 x fp16 split", exponent-shifted):

@@ -260,7 +260,8 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
   if (tid < 48) misc[tid] = 0.f;
   if (tid < 96 && Cin < 96 && tid >= Cin)  // pad rows of the W1 table
     for (int j = 0; j < 32; ++j) w1t[tid * 32 + j] = 0.f;
-  // pad channels [Cin, 96) of every X tile: never written by the staging
+  // pad channels [Cin, 96) of every X tile: the staging never writes them; batches > 256 overlay
+  // the partial table on the X slots, so pass 2 re-zeroes them after each exchange
   for (int r = tid; r < FIT_NW * FIT_SLOTS * 32; r += blockDim.x)
     for (int col = Cin; col < 96; ++col) lds[FIT_L_XS + r * FIT_XS + col] = 0.f;
   __syncthreads();
@@ -586,6 +587,8 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
     float dw2[3] = {0.f, 0.f, 0.f}, db1 = 0.f;
     // batch > 256: the partial table overlaid the X slots, so the tiles are gathered again
     // (pipelined as in pass 1) and their forward recomputed
+    if (bigbatch)  // the table overlaid this wave's 64 X rows (its readers are behind bsum5's barriers)
+      for (int col = Cin; col < 96; ++col) xs[lane * FIT_XS + col] = 0.f;
     if (!resident && tw > 0) fit_stage_pair(a, xs, srcp0, 0, Cin, lane);
     for (int i = 0; i < tw; ++i) {
       const int t = wave + FIT_NW * i;
@@ -808,8 +811,11 @@ extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
   if (batch < 1 || batch > FIT_MAX_BATCH) return 0;
   // partial table: the LDS union (resident X) or the X slots (batch > FIT_RES_BATCH)
   if (G * batch * 3 > (batch > FIT_RES_BATCH ? FIT_NW * FIT_SLOTS * FIT_XT : FIT_UNION)) return 0;
-  // the G working workgroups spin on each other's partials, so all must be resident at once: one
-  // per CU (LDS), on the XCD the blockIdx % 8 == 0 workgroups are dispatched to
+  // the G working workgroups spin on each other's partials, so all must be resident at once. The
+  // criterion does not depend on the XCD layout: the whole 8 G grid fits the device's resident
+  // capacity (occ per CU x CUs), so every workgroup is dispatched without waiting for another to
+  // finish. With 8 XCDs (MI355X) the blockIdx % 8 == 0 workers share one XCD; with another XCD
+  // count they do not, the launch-start check sees it and the exchange takes the sc1 path.
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -818,7 +824,7 @@ extern "C" int hpe_fit_supported(const hpe_program* p, int32_t batch) {
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, FIT_LDS_BYTES) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k, FIT_NW * 64, FIT_LDS_BYTES) != hipSuccess)
     return 0;
-  return occ >= 1 && G <= cus / 8;
+  return occ >= 1 && 8 * G <= occ * cus;
 }
 
 extern "C" size_t hpe_fit_workspace_size(const hpe_program* p, int32_t batch) {

@@ -1317,7 +1317,9 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
       const float* w2n = W2 + min(n, F - 1) * 3;
       const float s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
       const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
-      *(f32x4*)(colt + n * 4) = f32x4{SPLIT_INV_C / s1, b1, s2, 0.f};
+      // tanh: 2 log2(e) folded into the pre-activation affine (z' = 2 log2(e) z feeds exp2 directly)
+      const float kz = ACT1 == ACT_TANH ? 2.8853900817779268f : 1.f;
+      *(f32x4*)(colt + n * 4) = f32x4{(SPLIT_INV_C / s1) * kz, b1 * kz, s2, 0.f};
       *(f32x4*)(w2t + n * 4) = nok ? f32x4{w2n[0], w2n[1], w2n[2], 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
@@ -1433,7 +1435,8 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float zp = fmaf(acc[mb][nb][i], cs.x, cs.y);
-            float z = ACT1 == ACT_TANH ? fast_tanh5(zp) : act1_f<ACT1>(e1.act, zp);
+            float z = ACT1 == ACT_TANH ? fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(zp)), 1.f)
+                                       : act1_f<ACT1>(e1.act, zp);
             if (DROP) z = (dmask >> (12 * mb + 4 * nb + i)) & 1u ? z * inv_keep1 : 0.f;
             // act(0) = 0 for the compiled-in activations: units past F (zero W1 column, b1, W2
             // row) come out 0 without a mask
@@ -1552,7 +1555,9 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int nb = 0; nb < 3; ++nb) {
         const int n = n0 + 16 * nb;
-        const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
+        // W2 row scaled by the unit's power of two s2 (the dZ1 B-fragment scale): dA1, dZ1 and the
+        // db1 sum come out scaled by s2 exactly (unscaled at the flush)
+        const f32x4 w2v = *(const f32x4*)(w2t + n * 4) * colt[n * 4 + 2];
         f32x8 dv;
         f32x4 gsum = {0.f, 0.f, 0.f, 0.f};  // this tile's (dW2 row, db1) of the lane's 8 rows
         int zo = 0;
@@ -1571,12 +1576,13 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
             } else {
               gz = da;
             }
-            gz = n < F ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
+            // units past F: zero W2 row, so gz = 0 (act(0) = 0 for the compiled-in activations)
+            gz = (ACT1 >= 0 || n < F) ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
             gsum += f32x4{a * d.x, a * d.y, a * d.z, gz};
             dv[4 * mb + i] = gz;
           }
         *(f32x4*)(gme + 64 * nb) += gsum;
-        dsp[nb] = split_w8(dv * colt[n * 4 + 2]);
+        dsp[nb] = split_w8(dv);
       }
       VSTAMP(6);
       // stage X(t+2) only now: no LDS-DMA is in flight while head / backward rows run their LDS
@@ -1629,6 +1635,7 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
       const f32x4 gs = *(const f32x4*)(gme + 64 * nb);
       float tb = gs.w + __shfl_xor(gs.w, 16, 64);
       tb += xor32(tb);
+      tb *= 1.f / s2f;  // the db1 sums carry the unit's power-of-two scale s2 (exact)
       float t2[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
@@ -1794,6 +1801,9 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
   }
   hpe_tev_end(s);
   if (split_only()) return 0;
+  // inputs the caller bounds below the data-side range: the guard cannot fire (finite weights are
+  // scaled into range), so the exact twin's early-exit launch is not queued
+  if (a.x_bound > 0.f && a.x_bound < SPLIT_DATA_RANGE) return 0;
   return launch_k(pick(w), ncb, lds, a, grid, s);
 }
 

@@ -87,7 +87,12 @@ enum { BFH_MAGIC = 0, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF, BFH_WORDS = 8 };
 // BF_ROWS: a depthwise block streamed down the image in steps of TH output rows (ring of ROWS
 // input rows in LDS, next step's rows prefetched into registers); BFO_NI = row segments per image
 // BF_DIRECT: persistent, taps read from global, all output chunks per task (16x16 / 8x8 maps, heads)
-enum { BF_STEM = 1, BF_BLOCK = 2, BF_ROWS = 3, BF_DIRECT = 4 };
+// BF_STAGE: an execution record: the BFO_NI records after it (dw blocks on maps of <= 256
+// positions, and the detector heads right after the block producing their tap) run as ONE launch,
+// one workgroup per image, the map resident in LDS (bf_stage_kernel); BFO_CS = the map's channel
+// stride, BFO_ROWS / BFO_COLS = floats of the map / W^T regions, BFO_LDS = bytes.  The covered
+// records keep their per-op meaning (a reader that skips BF_STAGE computes the same outputs).
+enum { BF_STEM = 1, BF_BLOCK = 2, BF_ROWS = 3, BF_DIRECT = 4, BF_STAGE = 5 };
 enum { BF_RES_NONE = 0, BF_RES_ID = 1, BF_RES_MAXPOOL = 2 };
 // buffers: image input, two ping-pong activations, then the six caller outputs
 enum { BF_BUF_IMG = 0, BF_BUF_A = 1, BF_BUF_B = 2, BF_BUF_OUT0 = 3, BF_NBUF = 9 };

@@ -36,15 +36,25 @@
 #define RES_T 16                 // rows per block
 #define RES_SCR 640              // floats of a wave's transpose scratch: [2][16 rows][20]
 #define RES_MAXP 4096            // trainable parameters held in LDS
-#define RES_MAXSLOT 80           // per-lane partial-gradient slots (accumulators, bias sums, loss)
 #define RES_L_PRM 0
 #define RES_L_M (RES_L_PRM + RES_MAXP)    // fit: optimizer moments
 #define RES_L_V (RES_L_M + RES_MAXP)
 #define RES_L_SCR (RES_L_V + RES_MAXP)
 #define RES_L_RED (RES_L_SCR + RES_NW * RES_SCR)
-#define RES_L_MISC (RES_L_RED + 4 * RES_MAXSLOT * 64)
+#define RES_L_MISC (RES_L_RED + 4 * (RES_MAXP + 4))   // 4 flat partial-gradient copies
 #define RES_LDS_FLOATS (RES_L_MISC + 64)
 #define RES_LDS_BYTES (RES_LDS_FLOATS * 4)
+// the wide two-layer kernels (create_model 88 -> 64 -> 3: 5,891 parameters): more parameters in
+// LDS; the fit kernel's optimizer moments stay in the caller's global m / v (L2-resident, read and
+// written once per step by the optimizer, WIDE_MV per thread) instead of LDS
+#define WIDE_MAXP 6144
+#define WIDE_MV (WIDE_MAXP / (RES_NW * 64))
+#define WIDE_L_PRM 0
+#define WIDE_L_SCR (WIDE_L_PRM + WIDE_MAXP)
+#define WIDE_L_RED (WIDE_L_SCR + RES_NW * RES_SCR)
+#define WIDE_L_MISC (WIDE_L_RED + 4 * (WIDE_MAXP + 4))
+#define WIDE_LDS_BYTES ((WIDE_L_MISC + 64) * 4)
+static_assert(RES_LDS_BYTES <= 160 * 1024 && WIDE_LDS_BYTES <= 160 * 1024, "res LDS");
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -67,8 +77,6 @@ struct ResGeo {
   static constexpr int NL = 2 * NB + (BOTL ? 1 : 0) + 1;  // 16x16 layers after the first
   static constexpr int NLAY = NL + 1;
   static constexpr int NXB = (CIN + 15) / 16;             // 16-channel blocks of the first layer's dW
-  static constexpr int NSLOT = 4 * NXB + 4 * NL + NLAY + 2;
-  static_assert(NSLOT <= RES_MAXSLOT, "partial-gradient slots");
 };
 
 template <int KS, int NB, bool BOTL>
@@ -103,55 +111,123 @@ struct RowMap {
 // the layer activations on the hot path: softsign / tanh in a few VALU ops (reciprocal and exp
 // approximations, ~1-2 ulp), the rest as the interpreter computes them (act_f)
 __device__ __forceinline__ float res_act(int act, float z) {
+  if (act == ACT_LINEAR) return z;
   if (act == ACT_SOFTSIGN) return z * __builtin_amdgcn_rcpf(1.f + fabsf(z));
   if (act == ACT_TANH) return fast_tanh5(z);
   if (act == ACT_RELU) return z > 0.f ? z : 0.f;
   return act_f(act, z);
 }
+__device__ __forceinline__ float res_grad(int act, float a) {
+  if (act == ACT_LINEAR) return 1.f;
+  if (act == ACT_SOFTSIGN) {
+    const float t = 1.f - fabsf(a);
+    return t * t;
+  }
+  if (act == ACT_TANH) return 1.f - a * a;
+  if (act == ACT_RELU) return a > 0.f ? 1.f : 0.f;
+  return act_grad(act, a, 0.f);
+}
+
+// one dense layer: parameter offsets, K x N, activation, dropout (ordinal, threshold, 1 / keep)
+struct LD {
+  int wo, bo, K, N, act, drop;
+  uint32_t thr;
+  float ik;
+};
+
+// the layer table read ONCE per launch into registers (scalar loads of the program words inside the
+// step loop are re-issued after every LDS / global store the compiler cannot disambiguate).  HA >= 0:
+// the kernels compiled for create_model_complex's canonical geometry (first layer C_in x 16, blocks
+// 16 x 16, bottleneck 16 x 8, output x 3, parameters packed in layer order, every hidden layer HA,
+// the post-add activation relu, the output linear — checked on the host, res_fast): offsets, widths
+// and activations are compile-time constants, only the dropout words are read
+template <int KS, int NB, bool BOTL>
+struct ResDesc {
+  LD l[ResGeo<KS, NB, BOTL>::NLAY];
+  int post;
+};
+
+template <int KS, int NB, bool BOTL>
+__host__ __device__ constexpr int res_canon_k(int l) {
+  return l == 0 ? 4 * KS : (l == ResGeo<KS, NB, BOTL>::NLAY - 1 ? (BOTL ? 8 : 16) : 16);
+}
+template <int KS, int NB, bool BOTL>
+__host__ __device__ constexpr int res_canon_n(int l) {
+  return l == ResGeo<KS, NB, BOTL>::NLAY - 1 ? 3 : ((BOTL && l == 2 * NB + 1) ? 8 : 16);
+}
+template <int KS, int NB, bool BOTL>
+__host__ __device__ constexpr int res_canon_wo(int l) {
+  int o = 0;
+  for (int j = 0; j < l; ++j) o += res_canon_k<KS, NB, BOTL>(j) * res_canon_n<KS, NB, BOTL>(j) + res_canon_n<KS, NB, BOTL>(j);
+  return o;
+}
+
+template <int KS, int NB, bool BOTL, int HA>
+__device__ __forceinline__ ResDesc<KS, NB, BOTL> res_desc(const int* lt, int post) {
+  using G = ResGeo<KS, NB, BOTL>;
+  ResDesc<KS, NB, BOTL> D;
+#pragma unroll
+  for (int l = 0; l < G::NLAY; ++l) {
+    const int* e = lt + l * RL_WORDS;
+    LD& d = D.l[l];
+    if (HA >= 0) {
+      d.K = res_canon_k<KS, NB, BOTL>(l);
+      d.N = res_canon_n<KS, NB, BOTL>(l);
+      d.wo = res_canon_wo<KS, NB, BOTL>(l);
+      d.bo = d.wo + d.K * d.N;
+      d.act = l == G::NLAY - 1 ? ACT_LINEAR : HA;
+    } else {
+      d.K = e[RL_K];
+      d.N = e[RL_N];
+      d.wo = e[RL_W];
+      d.bo = e[RL_B];
+      d.act = e[RL_ACT];
+    }
+    d.drop = e[RL_DROP];
+    d.thr = (uint32_t)e[RL_THR];
+    d.ik = 1.f / __int_as_float(e[RL_KEEP]);
+  }
+  D.post = HA >= 0 ? ACT_RELU : post;
+  return D;
+}
 
 // one dense layer's R-layout epilogue: a = act(z + b) (0 past N), kept bits, y = dropout(a)
-__device__ __forceinline__ f4 res_epi(f4 z, const float* prm, const int* e, int g, uint64_t seed, uint64_t dimg,
-                                      f4& a, uint32_t& km) {
-  const int bo = e[RL_B], act = e[RL_ACT], drop = e[RL_DROP], N = e[RL_N];
-  const uint32_t thr = (uint32_t)e[RL_THR];
-  const float ik = 1.f / __int_as_float(e[RL_KEEP]);
-  const uint32_t base = drop >= 0 ? drop_base(seed, drop, dimg) : 0u;   // once per row and layer
+// (nb0: the first feature of this 16-wide output block of a wider layer)
+__device__ __forceinline__ f4 res_epi(f4 z, const float* prm, const LD& e, int g, uint64_t seed, uint64_t dimg,
+                                      f4& a, uint32_t& km, int nb0 = 0) {
+  const uint32_t base = e.drop >= 0 ? drop_base(seed, e.drop, dimg) : 0u;   // once per row and layer
   f4 y;
   km = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int n = 4 * g + i;
-    const float b = bo >= 0 ? prm[bo + min(n, N - 1)] : 0.f;
-    const float v = n < N ? res_act(act, z[i] + b) : 0.f;
+    const int n = nb0 + 4 * g + i;
+    const float b = e.bo >= 0 ? prm[e.bo + min(n, e.N - 1)] : 0.f;
+    const float v = n < e.N ? res_act(e.act, z[i] + b) : 0.f;
     a[i] = v;
     bool kp = true;
-    if (drop >= 0) kp = drop_mix(base, (uint32_t)n) >= thr;
+    if (e.drop >= 0) kp = drop_mix(base, (uint32_t)n) >= e.thr;
     km |= kp ? (1u << i) : 0u;
-    y[i] = kp ? (drop >= 0 ? v * ik : v) : 0.f;
+    y[i] = kp ? (e.drop >= 0 ? v * e.ik : v) : 0.f;
   }
   return y;
 }
 
 // y = dropout(a) again from the kept bits (the backward's layer input)
-__device__ __forceinline__ f4 res_redrop(f4 a, const int* e, uint32_t km) {
-  const int drop = e[RL_DROP];
-  const float ik = 1.f / __int_as_float(e[RL_KEEP]);
+__device__ __forceinline__ f4 res_redrop(f4 a, const LD& e, uint32_t km) {
   f4 y;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = (km >> i) & 1u ? (drop >= 0 ? a[i] * ik : a[i]) : 0.f;
+  for (int i = 0; i < 4; ++i) y[i] = (km >> i) & 1u ? (e.drop >= 0 ? a[i] * e.ik : a[i]) : 0.f;
   return y;
 }
 
 // dL/dz of a layer from dL/dy through its dropout and activation (csrc/hpe_common.h epi_bwd)
-__device__ __forceinline__ f4 res_epi_bwd(f4 dy, f4 a, const int* e, uint32_t km) {
-  const int act = e[RL_ACT], drop = e[RL_DROP];
-  const float ik = 1.f / __int_as_float(e[RL_KEEP]);
+__device__ __forceinline__ f4 res_epi_bwd(f4 dy, f4 a, const LD& e, uint32_t km) {
   f4 dz;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float gv = dy[i];
-    if (drop >= 0) gv = (km >> i) & 1u ? gv * ik : 0.f;
-    dz[i] = act == ACT_LINEAR ? gv : gv * act_grad(act, a[i], 0.f);
+    if (e.drop >= 0) gv = (km >> i) & 1u ? gv * e.ik : 0.f;
+    dz[i] = e.act == ACT_LINEAR ? gv : gv * res_grad(e.act, a[i]);
   }
   return dz;
 }
@@ -159,26 +235,25 @@ __device__ __forceinline__ f4 res_epi_bwd(f4 dy, f4 a, const int* e, uint32_t km
 // the weights are MFMA A operands read from the parameters in LDS at each use (all lanes of a
 // 16-lane group read consecutive or broadcast words: conflict-free), not held in registers
 // forward  Z^T = W^T . A^T: lane (g, c), K-step s: W[4g + s][c] (0 past K / N)
-__device__ __forceinline__ f4 res_fwd16(const float* prm, const int* e, int g, int c, f4 in) {
-  const int wo = e[RL_W], K = e[RL_K], N = e[RL_N];
-  f4 z = {0.f, 0.f, 0.f, 0.f};
+// (kb0 / nb0: the input / output block of a layer wider than 16; z: the accumulator to continue)
+__device__ __forceinline__ f4 res_fwd16(const float* prm, const LD& e, int g, int c, f4 in, int kb0 = 0, int nb0 = 0,
+                                        f4 z = f4{0.f, 0.f, 0.f, 0.f}) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int k = 4 * g + s;
-    const float w = prm[wo + min(k, K - 1) * N + min(c, N - 1)];
-    z = mfma4((k < K && c < N) ? w : 0.f, in[s], z);
+    const int k = kb0 + 4 * g + s, n = nb0 + c;
+    const float w = prm[e.wo + min(k, e.K - 1) * e.N + min(n, e.N - 1)];
+    z = mfma4((k < e.K && n < e.N) ? w : 0.f, in[s], z);
   }
   return z;
 }
 // backward dA^T = W . dZ^T: lane (g, c), K-step s: W[c][4g + s]
-__device__ __forceinline__ f4 res_bwd16(const float* prm, const int* e, int g, int c, f4 dz) {
-  const int wo = e[RL_W], K = e[RL_K], N = e[RL_N];
+__device__ __forceinline__ f4 res_bwd16(const float* prm, const LD& e, int g, int c, f4 dz, int kb0 = 0, int nb0 = 0) {
   f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int n = 4 * g + s;
-    const float w = prm[wo + min(c, K - 1) * N + min(n, N - 1)];
-    d = mfma4((c < K && n < N) ? w : 0.f, dz[s], d);
+    const int n = nb0 + 4 * g + s, k = kb0 + c;
+    const float w = prm[e.wo + min(k, e.K - 1) * e.N + min(n, e.N - 1)];
+    d = mfma4((k < e.K && n < e.N) ? w : 0.f, dz[s], d);
   }
   return d;
 }
@@ -205,16 +280,18 @@ __device__ __forceinline__ void res_dw16(f4& acc, float& dbp, f4 a_r, f4 dz_r, f
 
 // forward + loss + backward of one 16-row block starting at batch row R0
 template <int KS, int NB, bool BOTL>
-__device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const float* prm, const int* lt, int post,
-                                          const float* __restrict__ x, const float* __restrict__ ytrue,
-                                          const RowMap& rm, int64_t R0, uint64_t seed, float inv_count,
-                                          float* scr, int g, int c) {
+__device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const ResDesc<KS, NB, BOTL>& D,
+                                          const float* prm, const float* __restrict__ x,
+                                          const float* __restrict__ ytrue, const RowMap& rm, int64_t R0,
+                                          uint64_t seed, float inv_count, float* scr, int g, int c) {
   using G = ResGeo<KS, NB, BOTL>;
   constexpr int CIN = G::CIN;
   const int64_t Rc = R0 + c;
   const bool valid = Rc < rm.nrows;
   const int64_t Rl = valid ? Rc : rm.nrows - 1;
   const uint64_t dimg = rm.dimg(Rl);
+  const LD& e0 = D.l[0];
+  const LD& eo = D.l[G::NLAY - 1];
 
   // ---- forward: first layer from HBM (row c, channels KS g .. KS g + KS - 1)
   f4 a0, y0;
@@ -228,11 +305,11 @@ __device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const float
       xr[s] = v.x;
       xr[s + 1] = v.y;
     }
-    const float* w0 = prm + lt[RL_W] + KS * g * 16 + c;   // W0[KS g + s][c]
+    const float* w0 = prm + e0.wo + KS * g * 16 + c;   // W0[KS g + s][c]
     f4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) z = mfma4(w0[16 * s], xr[s], z);
-    y0 = res_epi(z, prm, lt, g, seed, dimg, a0, m0);
+    y0 = res_epi(z, prm, e0, g, seed, dimg, a0, m0);
   }
   RSTAMP(0);
   // the first layer's dW reads the input in T-layout (rows 4g + s, channels 16 b + c): issued
@@ -255,20 +332,19 @@ __device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const float
   f4 h = y0;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int* e1 = lt + (2 * b + 1) * RL_WORDS;
-    const int* e2 = lt + (2 * b + 2) * RL_WORDS;
+    const LD& e1 = D.l[2 * b + 1];
+    const LD& e2 = D.l[2 * b + 2];
     const f4 y1 = res_epi(res_fwd16(prm, e1, g, c, h), prm, e1, g, seed, dimg, a1[b], m1[b]);
     const f4 y2 = res_epi(res_fwd16(prm, e2, g, c, y1), prm, e2, g, seed, dimg, a2[b], m2[b]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ho[b][i] = res_act(post, h[i] + y2[i]);
+    for (int i = 0; i < 4; ++i) ho[b][i] = res_act(D.post, h[i] + y2[i]);
     h = ho[b];
   }
   // ---- bottleneck, output
   f4 ab = {0.f, 0.f, 0.f, 0.f}, yb = h;
   uint32_t mb = 0;
-  const int* eb = lt + (2 * NB + 1) * RL_WORDS;
+  const LD& eb = D.l[BOTL ? 2 * NB + 1 : 0];
   if (BOTL) yb = res_epi(res_fwd16(prm, eb, g, c, h), prm, eb, g, seed, dimg, ab, mb);
-  const int* eo = lt + G::NL * RL_WORDS;
   f4 ao;
   uint32_t mo;
   const f4 out = res_epi(res_fwd16(prm, eo, g, c, yb), prm, eo, g, seed, dimg, ao, mo);
@@ -298,11 +374,11 @@ __device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const float
   }
 #pragma unroll
   for (int b = NB - 1; b >= 0; --b) {
-    const int* e1 = lt + (2 * b + 1) * RL_WORDS;
-    const int* e2 = lt + (2 * b + 2) * RL_WORDS;
+    const LD& e1 = D.l[2 * b + 1];
+    const LD& e2 = D.l[2 * b + 2];
     f4 ds;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ds[i] = post == ACT_LINEAR ? dh[i] : dh[i] * act_grad(post, ho[b][i], 0.f);
+    for (int i = 0; i < 4; ++i) ds[i] = D.post == ACT_LINEAR ? dh[i] : dh[i] * res_grad(D.post, ho[b][i]);
     const f4 dz2 = res_epi_bwd(ds, a2[b], e2, m2[b]);
     res_dw16(S.acc[2 * b + 1], S.dbp[2 * b + 2], res_redrop(a1[b], e1, m1[b]), dz2, scr, g, c);
     const f4 dz1 = res_epi_bwd(res_bwd16(prm, e2, g, c, dz2), a1[b], e1, m1[b]);
@@ -314,7 +390,7 @@ __device__ __forceinline__ void res_block(ResState<KS, NB, BOTL>& S, const float
   RSTAMP(2);
   // ---- first layer: dW0 += X^T . dZ0
   {
-    const f4 dz0 = res_epi_bwd(dh, a0, lt, m0);
+    const f4 dz0 = res_epi_bwd(dh, a0, e0, m0);
     float dt[4];
     res_to_t(scr + 320, dz0, g, c, dt);
 #pragma unroll
@@ -339,127 +415,291 @@ __device__ __forceinline__ void res_zero(ResState<KS, NB, BOTL>& S) {
   S.sae = 0.f;
 }
 
-// the workgroup's 8 partial gradients summed into wave 0 in a fixed order:
-// ((w0 + w4) + (w2 + w6)) + ((w1 + w5) + (w3 + w7)); slot-major [slot][64 lanes] in LDS
-template <int KS, int NB, bool BOTL>
-__device__ __forceinline__ void res_tree(ResState<KS, NB, BOTL>& S, float* red, int wave, int lane) {
+// a wave's partial gradient in the flat parameter layout: every trainable parameter of the stack
+// is one dW / bias entry, so the wave writes (ADD = false) or adds onto (ADD = true) every word of
+// out[0 .. npt) once, and out[npt], out[npt + 1] (sse, sae)
+template <int KS, int NB, bool BOTL, bool ADD>
+__device__ __forceinline__ void res_flat(const ResState<KS, NB, BOTL>& S, const ResDesc<KS, NB, BOTL>& D, float* out,
+                                         int npt, int g, int c, int lane) {
   using G = ResGeo<KS, NB, BOTL>;
-#pragma unroll 1
-  for (int st = 4; st >= 1; st >>= 1) {
-    if (wave >= st && wave < 2 * st) {
-      float* r = red + (wave - st) * RES_MAXSLOT * 64 + lane;
-      int k = 0;
+#define RES_PUT(idx, v) do { float* p_ = out + (idx); *p_ = ADD ? *p_ + (v) : (v); } while (0)
 #pragma unroll
-      for (int b = 0; b < G::NXB; ++b)
+  for (int b = 0; b < G::NXB; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[64 * k++] = S.acc0[b][i];
-#pragma unroll
-      for (int l = 0; l < G::NL; ++l)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[64 * k++] = S.acc[l][i];
-#pragma unroll
-      for (int l = 0; l < G::NLAY; ++l) r[64 * k++] = S.dbp[l];
-      r[64 * k++] = S.sse;
-      r[64 * k++] = S.sae;
+    for (int i = 0; i < 4; ++i) {
+      const int in = 16 * b + 4 * g + i;
+      if (in < G::CIN) RES_PUT(D.l[0].wo + in * 16 + c, S.acc0[b][i]);
     }
-    __syncthreads();
-    if (wave < st) {
-      const float* r = red + wave * RES_MAXSLOT * 64 + lane;
-      int k = 0;
-#pragma unroll
-      for (int b = 0; b < G::NXB; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) S.acc0[b][i] += r[64 * k++];
-#pragma unroll
-      for (int l = 0; l < G::NL; ++l)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) S.acc[l][i] += r[64 * k++];
-#pragma unroll
-      for (int l = 0; l < G::NLAY; ++l) S.dbp[l] += r[64 * k++];
-      S.sse += r[64 * k++];
-      S.sae += r[64 * k++];
-    }
-    __syncthreads();
-  }
-}
-
-// wave 0 after the tree: the flat gradient [n_train] (+ sse, sae at out[npt], out[npt + 1])
-template <int KS, int NB, bool BOTL>
-__device__ __forceinline__ void res_emit(ResState<KS, NB, BOTL>& S, const int* lt, float* out, int npt, int g, int c,
-                                         int lane) {
-  using G = ResGeo<KS, NB, BOTL>;
-  {
-    const int wo = lt[RL_W];
-#pragma unroll
-    for (int b = 0; b < G::NXB; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int in = 16 * b + 4 * g + i;
-        if (in < G::CIN) out[wo + in * 16 + c] = S.acc0[b][i];
-      }
-  }
 #pragma unroll
   for (int l = 0; l < G::NL; ++l) {
-    const int* e = lt + (l + 1) * RL_WORDS;
-    const int wo = e[RL_W], K = e[RL_K], N = e[RL_N];
+    const LD& e = D.l[l + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int in = 4 * g + i;
-      if (in < K && c < N) out[wo + in * N + c] = S.acc[l][i];
+      if (in < e.K && c < e.N) RES_PUT(e.wo + in * e.N + c, S.acc[l][i]);
     }
   }
 #pragma unroll
   for (int l = 0; l < G::NLAY; ++l) {
-    const int* e = lt + l * RL_WORDS;
+    const LD& e = D.l[l];
     float v = S.dbp[l];
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
-    if (g == 0 && e[RL_B] >= 0 && c < e[RL_N]) out[e[RL_B] + c] = v;
+    if (g == 0 && e.bo >= 0 && c < e.N) RES_PUT(e.bo + c, v);
   }
   const float a = wave_sum(S.sse), b = wave_sum(S.sae);
   if (lane == 0) {
-    out[npt] = a;
-    out[npt + 1] = b;
+    RES_PUT(npt, a);
+    RES_PUT(npt + 1, b);
+  }
+#undef RES_PUT
+}
+
+// the workgroup's 8 partial gradients: waves 4..7 write flat copies 0..3, waves 0..3 add theirs onto
+// copy w, then every parameter i is ((c0 + c1) + (c2 + c3))[i] — a fixed order, identical in the
+// per-step and whole-epoch kernels (bit-identical paths); returns after the barrier that publishes
+template <int KS, int NB, bool BOTL>
+__device__ __forceinline__ void res_reduce(const ResState<KS, NB, BOTL>& S, const ResDesc<KS, NB, BOTL>& D,
+                                           float* cp, int npt, int stride, int wave, int g, int c, int lane) {
+  if (wave >= 4) res_flat<KS, NB, BOTL, false>(S, D, cp + (wave - 4) * stride, npt, g, c, lane);
+  __syncthreads();
+  if (wave < 4) res_flat<KS, NB, BOTL, true>(S, D, cp + wave * stride, npt, g, c, lane);
+  __syncthreads();
+}
+
+__device__ __forceinline__ float res_sum4(const float* cp, int stride, int i) {
+  return (cp[i] + cp[stride + i]) + (cp[2 * stride + i] + cp[3 * stride + i]);
+}
+
+// ================================================================================================
+// The same machinery for the 2-layer create_model family with a narrow hidden layer (train_88.py
+// :66-140 create_model: 88 -> 64 softsign -> 3, configs[2]'s Model-88 training at batch 512, and any
+// F <= 64 multiple of 16): x -> dense F (act, dropout) -> dense 3 (act, dropout).  The hidden layer
+// is FB = F / 16 R-layout blocks; the output layer's K runs over them.  Used for P = 1 training
+// launches and the whole-epoch kernel (P > 1 launches keep mlp2_kernel, which tiles 32 rows x all
+// units per workgroup for the large-map lines).
+// ================================================================================================
+template <int KS, int FB>
+struct WideState {
+  f4 acc0[(4 * KS + 15) / 16][FB];   // dW0[16 b + 4g + i][16 bn + c]
+  f4 acco[FB];                       // dWo[16 bk + 4g + i][c]
+  float db0[FB], dbo;
+  float sse, sae;
+};
+
+template <int KS, int FB>
+__device__ __forceinline__ void wide_zero(WideState<KS, FB>& S) {
+#pragma unroll
+  for (int b = 0; b < (4 * KS + 15) / 16; ++b)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) S.acc0[b][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < FB; ++j) {
+    S.acco[j] = f4{0.f, 0.f, 0.f, 0.f};
+    S.db0[j] = 0.f;
+  }
+  S.dbo = S.sse = S.sae = 0.f;
+}
+
+// layer descriptors: HA >= 0 (create_model's canonical packing: W0 [C_in][F], b0, W1 [F][3], b1;
+// the hidden activation HA, the output linear) or the program's runtime words
+template <int KS, int FB, int HA>
+__device__ __forceinline__ void wide_desc(const int* lt, LD& e0, LD& eo) {
+  const int* t[2] = {lt, lt + RL_WORDS};
+  LD* d[2] = {&e0, &eo};
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    const int* e = t[l];
+    if (HA >= 0) {
+      d[l]->K = l == 0 ? 4 * KS : 16 * FB;
+      d[l]->N = l == 0 ? 16 * FB : 3;
+      d[l]->wo = l == 0 ? 0 : 4 * KS * 16 * FB + 16 * FB;
+      d[l]->bo = d[l]->wo + d[l]->K * d[l]->N;
+      d[l]->act = l == 0 ? HA : ACT_LINEAR;
+    } else {
+      d[l]->K = e[RL_K];
+      d[l]->N = e[RL_N];
+      d[l]->wo = e[RL_W];
+      d[l]->bo = e[RL_B];
+      d[l]->act = e[RL_ACT];
+    }
+    d[l]->drop = e[RL_DROP];
+    d[l]->thr = (uint32_t)e[RL_THR];
+    d[l]->ik = 1.f / __int_as_float(e[RL_KEEP]);
   }
 }
 
-// The file is compiled three times (csrc/Makefile): RES_PART 88 / 96 instantiate the kernels of one
-// input width, RES_PART 0 the host dispatch (the kernel instantiations take minutes to compile).
+template <int KS, int FB>
+__device__ __forceinline__ void wide_block(WideState<KS, FB>& S, const LD& e0, const LD& eo, const float* prm,
+                                           const float* __restrict__ x, const float* __restrict__ ytrue,
+                                           const RowMap& rm, int64_t R0, uint64_t seed, float inv_count, float* scr,
+                                           int g, int c) {
+  constexpr int CIN = 4 * KS, NXB = (CIN + 15) / 16;
+  const int64_t Rc = R0 + c;
+  const bool valid = Rc < rm.nrows;
+  const int64_t Rl = valid ? Rc : rm.nrows - 1;
+  const uint64_t dimg = rm.dimg(Rl);
+  // ---- hidden layer: FB output blocks, K = C_in from HBM
+  f4 a0[FB], h[FB];
+  uint32_t m0[FB];
+  {
+    const float* xp = x + rm.src(Rl) * CIN + KS * g;
+    float xr[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s += 2) {
+      const float2 v = *(const float2*)(xp + s);
+      xr[s] = v.x;
+      xr[s + 1] = v.y;
+    }
+    const float* w0 = prm + e0.wo + KS * g * e0.N + c;   // W0[KS g + s][16 bn + c]
+#pragma unroll
+    for (int bn = 0; bn < FB; ++bn) {
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) z = mfma4(w0[s * e0.N + 16 * bn], xr[s], z);
+      h[bn] = res_epi(z, prm, e0, g, seed, dimg, a0[bn], m0[bn], 16 * bn);
+    }
+  }
+  float xt[NXB][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t R = min(R0 + 4 * g + s, rm.nrows - 1);
+    const float* xp = x + rm.src(R) * CIN;
+#pragma unroll
+    for (int b = 0; b < NXB; ++b) {
+      const int ch = 16 * b + c;
+      const float v = xp[min(ch, CIN - 1)];
+      xt[b][s] = ch < CIN ? v : 0.f;
+    }
+  }
+  // ---- output layer: K = F over the FB blocks
+  f4 zo = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int bk = 0; bk < FB; ++bk) zo = res_fwd16(prm, eo, g, c, h[bk], 16 * bk, 0, zo);
+  f4 ao;
+  uint32_t mo;
+  const f4 out = res_epi(zo, prm, eo, g, seed, dimg, ao, mo);
+  f4 dout = {0.f, 0.f, 0.f, 0.f};
+  if (g == 0 && valid) {
+    const float* yl = ytrue + rm.label(Rl) * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float err = out[i] - yl[i];
+      S.sse = fmaf(err, err, S.sse);
+      S.sae += fabsf(err);
+      dout[i] = 2.f * err * inv_count;
+    }
+  }
+  // ---- backward
+  const f4 dz = res_epi_bwd(dout, ao, eo, mo);
+  float dt[4];
+  res_to_t(scr + 320, dz, g, c, dt);
+  S.dbo += (dt[0] + dt[1]) + (dt[2] + dt[3]);
+#pragma unroll
+  for (int bk = 0; bk < FB; ++bk) {
+    float at[4];
+    res_to_t(scr, h[bk], g, c, at);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) S.acco[bk] = mfma4(at[s], dt[s], S.acco[bk]);
+  }
+#pragma unroll
+  for (int bk = 0; bk < FB; ++bk) {
+    const f4 dz1 = res_epi_bwd(res_bwd16(prm, eo, g, c, dz, 16 * bk, 0), a0[bk], e0, m0[bk]);
+    float d1[4];
+    res_to_t(scr, dz1, g, c, d1);
+#pragma unroll
+    for (int b = 0; b < NXB; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) S.acc0[b][bk] = mfma4(xt[b][s], d1[s], S.acc0[b][bk]);
+    S.db0[bk] += (d1[0] + d1[1]) + (d1[2] + d1[3]);
+  }
+}
+
+template <int KS, int FB, bool ADD>
+__device__ __forceinline__ void wide_flat(const WideState<KS, FB>& S, const LD& e0, const LD& eo, float* out, int npt,
+                                          int g, int c, int lane) {
+  constexpr int CIN = 4 * KS, NXB = (CIN + 15) / 16;
+#define RES_PUT(idx, v) do { float* p_ = out + (idx); *p_ = ADD ? *p_ + (v) : (v); } while (0)
+#pragma unroll
+  for (int b = 0; b < NXB; ++b)
+#pragma unroll
+    for (int bn = 0; bn < FB; ++bn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int in = 16 * b + 4 * g + i, n = 16 * bn + c;
+        if (in < CIN && n < e0.N) RES_PUT(e0.wo + in * e0.N + n, S.acc0[b][bn][i]);
+      }
+#pragma unroll
+  for (int bk = 0; bk < FB; ++bk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int in = 16 * bk + 4 * g + i;
+      if (in < eo.K && c < eo.N) RES_PUT(eo.wo + in * eo.N + c, S.acco[bk][i]);
+    }
+#pragma unroll
+  for (int bn = 0; bn < FB; ++bn) {
+    float v = S.db0[bn];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (g == 0 && e0.bo >= 0 && 16 * bn + c < e0.N) RES_PUT(e0.bo + 16 * bn + c, v);
+  }
+  {
+    float v = S.dbo;
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (g == 0 && eo.bo >= 0 && c < eo.N) RES_PUT(eo.bo + c, v);
+  }
+  const float a = wave_sum(S.sse), b = wave_sum(S.sae);
+  if (lane == 0) {
+    RES_PUT(npt, a);
+    RES_PUT(npt + 1, b);
+  }
+#undef RES_PUT
+}
+
+template <int KS, int FB>
+__device__ __forceinline__ void wide_reduce(const WideState<KS, FB>& S, const LD& e0, const LD& eo, float* cp, int npt,
+                                            int stride, int wave, int g, int c, int lane) {
+  if (wave >= 4) wide_flat<KS, FB, false>(S, e0, eo, cp + (wave - 4) * stride, npt, g, c, lane);
+  __syncthreads();
+  if (wave < 4) wide_flat<KS, FB, true>(S, e0, eo, cp + wave * stride, npt, g, c, lane);
+  __syncthreads();
+}
+
+// The file is compiled five times (csrc/Makefile): RES_PART 88 / 96 with RES_FAST 0 / 1 instantiate
+// the kernels of one input width and activation set, RES_PART 0 the host dispatch (the kernel
+// instantiations take minutes to compile).
 #ifndef RES_PART
 #define RES_PART 0
 #endif
 
-// ---- hpe_train_step: per-workgroup gradient slabs -------------------------------------------------
-template <int KS, int NB, bool BOTL>
+// ---- hpe_train_step: per-workgroup gradient slabs ---------------------------------------------
+template <int KS, int NB, bool BOTL, int HA>
 __global__ void __launch_bounds__(RES_NW * 64) res_train_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* prog = a.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int* lt = prog + o[O_AUX0];
-  const int post = o[O_MODE];
   const int npt = prog[H_NPARAMS_TRAIN];
+  const int stride = (npt + 4 + 3) & ~3;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   float* prm = lds + RES_L_PRM;
   float* scr = lds + RES_L_SCR + wave * RES_SCR;
-  float* red = lds + RES_L_RED;
+  float* cp = lds + RES_L_RED;
   for (int i = threadIdx.x; i < npt; i += RES_NW * 64) prm[i] = a.params[i];
+  const ResDesc<KS, NB, BOTL> D = res_desc<KS, NB, BOTL, HA>(lt, o[O_MODE]);
   __syncthreads();
   ResState<KS, NB, BOTL> S;
   res_zero(S);
   RowMap rm = {a.idx, nullptr, 0, a.nrows, a.img_off, a.P, false};
   const int64_t nblk = (a.nrows + RES_T - 1) / RES_T;
   for (int64_t blk = (int64_t)blockIdx.x * RES_NW + wave; blk < nblk; blk += (int64_t)gridDim.x * RES_NW)
-    res_block(S, prm, lt, post, a.x, a.ytrue, rm, blk * RES_T, a.seed, a.inv_count, scr, g, c);
-  res_tree(S, red, wave, lane);
-  if (wave == 0) {
-    float* ws = a.ws + (size_t)blockIdx.x * prog[H_SLAB];
-    res_emit(S, lt, ws, npt, g, c, lane);
-    if (lane == 0) {
-      ws[npt + 2] = 0.f;
-      ws[npt + 3] = 0.f;
-    }
-  }
+    res_block(S, D, prm, a.x, a.ytrue, rm, blk * RES_T, a.seed, a.inv_count, scr, g, c);
+  res_reduce(S, D, cp, npt, stride, wave, g, c, lane);
+  float* ws = a.ws + (size_t)blockIdx.x * prog[H_SLAB];
+  for (int i = threadIdx.x; i < npt + 2; i += RES_NW * 64) ws[i] = res_sum4(cp, stride, i);
+  if (threadIdx.x < 2) ws[npt + 2 + threadIdx.x] = 0.f;
 }
 
 // ---- hpe_fit_epoch: the whole epoch in one workgroup ------------------------------------------------
@@ -484,14 +724,85 @@ struct ResFitArgs {
   int* flags;               // workspace word 1 (always 0: exact fp32 throughout)
 };
 
-template <int KS, int NB, bool BOTL>
+// one step of the Keras legacy optimizer over the workgroup's parameters in LDS from the summed
+// flat gradient copies (hpe_rowprog.hip optim_update with gscale 1: the same float operations), the
+// regularisation loss on the pre-update weights, and the step's stats row
+__device__ __forceinline__ float res_opt_one(const ResFitArgs& a, float alpha, float wi, float c2, float g,
+                                             float& mi, float& vi) {
+  const float gr = fmaf(g, 1.f, 2.f * c2 * wi);
+  if (a.kind == HPE_OPT_SGD) return wi - alpha * gr;
+  if (a.kind == HPE_OPT_ADAM) {
+    mi += (gr - mi) * (1.f - a.b1);
+    vi += (gr * gr - vi) * (1.f - a.b2);
+    return wi - (mi * alpha) / (sqrtf(vi) + a.eps);
+  }
+  mi += (gr - mi) * (1.f - a.b1);
+  vi = fmaxf(a.b2 * vi, fabsf(gr));
+  return wi - alpha * (mi / (vi + a.eps));
+}
+
+// GM: the optimizer moments are the caller's global a.m / a.v (all of a thread's loads issued
+// before the first use), not LDS mom / vel
+template <bool GM>
+__device__ __forceinline__ void res_opt_step(const ResFitArgs& a, float* prm, float* mom, float* vel, const float* cp,
+                                             int stride, int npt, int s, float* misc, int tid, int lane, int wave) {
+  const float alpha = a.alpha[s];
+  float reg = 0.f;
+  if (GM) {
+    float mr[WIDE_MV], vr[WIDE_MV];
+    const bool mv = a.kind != HPE_OPT_SGD;
+#pragma unroll
+    for (int k = 0; k < WIDE_MV; ++k) {
+      const int i = tid + k * RES_NW * 64;
+      mr[k] = mv && i < npt ? a.m[i] : 0.f;
+      vr[k] = mv && i < npt ? a.v[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < WIDE_MV; ++k) {
+      const int i = tid + k * RES_NW * 64;
+      if (i < npt) {
+        const float wi = prm[i], c2 = a.l2[i];
+        reg = fmaf(c2 * wi, wi, reg);
+        prm[i] = res_opt_one(a, alpha, wi, c2, res_sum4(cp, stride, i), mr[k], vr[k]);
+        if (mv) {
+          a.m[i] = mr[k];
+          a.v[i] = vr[k];
+        }
+      }
+    }
+  } else {
+    for (int i = tid; i < npt; i += RES_NW * 64) {
+      const float wi = prm[i], c2 = a.l2[i];
+      reg = fmaf(c2 * wi, wi, reg);
+      float mi = mom[i], vi = vel[i];
+      prm[i] = res_opt_one(a, alpha, wi, c2, res_sum4(cp, stride, i), mi, vi);
+      if (a.kind != HPE_OPT_SGD) {
+        mom[i] = mi;
+        vel[i] = vi;
+      }
+    }
+  }
+  reg = wave_sum(reg);
+  if (lane == 0) misc[wave] = reg;
+  // the copies are read before the barrier (the next step's reduction overwrites them after it)
+  const float sse = res_sum4(cp, stride, npt), sae = res_sum4(cp, stride, npt + 1);
+  __syncthreads();
+  if (tid == 0) {
+    float* st = a.stats + (size_t)s * a.stats_stride;
+    st[0] = sse;
+    st[1] = sae;
+    st[2] = ((misc[0] + misc[1]) + (misc[2] + misc[3])) + ((misc[4] + misc[5]) + (misc[6] + misc[7]));
+  }
+}
+
+template <int KS, int NB, bool BOTL, int HA>
 __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* prog = a.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int* lt = prog + o[O_AUX0];
-  const int post = o[O_MODE];
   const int npt = prog[H_NPARAMS_TRAIN];
+  const int stride = (npt + 4 + 3) & ~3;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int tid = threadIdx.x;
@@ -499,7 +810,7 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
   float* mom = lds + RES_L_M;
   float* vel = lds + RES_L_V;
   float* scr = lds + RES_L_SCR + wave * RES_SCR;
-  float* red = lds + RES_L_RED;
+  float* cp = lds + RES_L_RED;
   float* misc = lds + RES_L_MISC;
   for (int i = tid; i < npt; i += RES_NW * 64) {
     prm[i] = a.params[i];
@@ -507,6 +818,7 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
     vel[i] = a.kind != HPE_OPT_SGD ? a.v[i] : 0.f;
   }
   if (tid == 0) a.flags[1] = 0;
+  const ResDesc<KS, NB, BOTL> D = res_desc<KS, NB, BOTL, HA>(lt, o[O_MODE]);
   __syncthreads();
   ResState<KS, NB, BOTL> S;
 #ifdef RES_STAMPS
@@ -524,58 +836,17 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
     const float inv = 1.f / (float)(nb * 3);
     const int nblk = (nb + RES_T - 1) / RES_T;
     for (int blk = wave; blk < nblk; blk += RES_NW)
-      res_block(S, prm, lt, post, a.x, a.ytrue, rm, (int64_t)blk * RES_T, seed, inv, scr, g, c);
-    res_tree(S, red, wave, lane);
+      res_block(S, D, prm, a.x, a.ytrue, rm, (int64_t)blk * RES_T, seed, inv, scr, g, c);
+    res_reduce(S, D, cp, npt, stride, wave, g, c, lane);
     RSTAMP(4);
-    // wave 0: the step's flat gradient into LDS (over the tree buffer, free after the last barrier)
-    if (wave == 0) res_emit(S, lt, red, npt, g, c, lane);
-    __syncthreads();
+    res_opt_step<false>(a, prm, mom, vel, cp, stride, npt, s, misc, tid, lane, wave);
     RSTAMP(5);
-    // Keras legacy optimizer (hpe_rowprog.hip optim_update with gscale 1: the same float operations)
-    const float alpha = a.alpha[s];
-    float reg = 0.f;
-    for (int i = tid; i < npt; i += RES_NW * 64) {
-      const float wi = prm[i], c2 = a.l2[i];
-      reg = fmaf(c2 * wi, wi, reg);
-      const float gr = fmaf(red[i], 1.f, 2.f * c2 * wi);
-      float wn;
-      if (a.kind == HPE_OPT_SGD) {
-        wn = wi - alpha * gr;
-      } else if (a.kind == HPE_OPT_ADAM) {
-        float mi = mom[i], vi = vel[i];
-        mi += (gr - mi) * (1.f - a.b1);
-        vi += (gr * gr - vi) * (1.f - a.b2);
-        mom[i] = mi;
-        vel[i] = vi;
-        wn = wi - (mi * alpha) / (sqrtf(vi) + a.eps);
-      } else {
-        float mi = mom[i], vi = vel[i];
-        mi += (gr - mi) * (1.f - a.b1);
-        vi = fmaxf(a.b2 * vi, fabsf(gr));
-        mom[i] = mi;
-        vel[i] = vi;
-        wn = wi - alpha * (mi / (vi + a.eps));
-      }
-      prm[i] = wn;
-    }
-    reg = wave_sum(reg);
-    if (lane == 0) misc[wave] = reg;
-    __syncthreads();
-    if (tid == 0) {
-      float* st = a.stats + (size_t)s * a.stats_stride;
-      st[0] = red[npt];
-      st[1] = red[npt + 1];
-      st[2] = ((misc[0] + misc[1]) + (misc[2] + misc[3])) + ((misc[4] + misc[5]) + (misc[6] + misc[7]));
-    }
-    __syncthreads();  // the gradient buffer is the next step's tree buffer
-    RSTAMP(6);
   }
 #ifdef RES_STAMPS
   if (threadIdx.x == 0)
-    printf("RSTAMP steps %d: fwd0 %llu fwd %llu bwd %llu dw0 %llu tree %llu emit %llu opt %llu\n", a.steps,
+    printf("RSTAMP steps %d: fwd0 %llu fwd %llu bwd %llu dw0 %llu reduce %llu opt %llu\n", a.steps,
            (unsigned long long)g_rst[0], (unsigned long long)g_rst[1], (unsigned long long)g_rst[2],
-           (unsigned long long)g_rst[3], (unsigned long long)g_rst[4], (unsigned long long)g_rst[5],
-           (unsigned long long)g_rst[6]);
+           (unsigned long long)g_rst[3], (unsigned long long)g_rst[4], (unsigned long long)g_rst[5]);
 #endif
   for (int i = tid; i < npt; i += RES_NW * 64) {
     const float w = prm[i];
@@ -589,47 +860,167 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
   }
 }
 
+// ---- the wide two-layer kernels: same launch shapes, LDS layout and reduction order -----------------
+template <int KS, int FB, int HA>
+__global__ void __launch_bounds__(RES_NW * 64) wide_train_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int* prog = a.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int* lt = prog + o[O_AUX0];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  const int stride = (npt + 4 + 3) & ~3;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  float* prm = lds + WIDE_L_PRM;
+  float* scr = lds + WIDE_L_SCR + wave * RES_SCR;
+  float* cp = lds + WIDE_L_RED;
+  for (int i = threadIdx.x; i < npt; i += RES_NW * 64) prm[i] = a.params[i];
+  LD e0, eo;
+  wide_desc<KS, FB, HA>(lt, e0, eo);
+  __syncthreads();
+  WideState<KS, FB> S;
+  wide_zero(S);
+  RowMap rm = {a.idx, nullptr, 0, a.nrows, a.img_off, a.P, false};
+  const int64_t nblk = (a.nrows + RES_T - 1) / RES_T;
+  for (int64_t blk = (int64_t)blockIdx.x * RES_NW + wave; blk < nblk; blk += (int64_t)gridDim.x * RES_NW)
+    wide_block(S, e0, eo, prm, a.x, a.ytrue, rm, blk * RES_T, a.seed, a.inv_count, scr, g, c);
+  wide_reduce(S, e0, eo, cp, npt, stride, wave, g, c, lane);
+  float* ws = a.ws + (size_t)blockIdx.x * prog[H_SLAB];
+  for (int i = threadIdx.x; i < npt + 2; i += RES_NW * 64) ws[i] = res_sum4(cp, stride, i);
+  if (threadIdx.x < 2) ws[npt + 2 + threadIdx.x] = 0.f;
+}
+
+template <int KS, int FB, int HA>
+__global__ void __launch_bounds__(RES_NW * 64) wide_fit_kernel(ResFitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int* prog = a.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int* lt = prog + o[O_AUX0];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  const int stride = (npt + 4 + 3) & ~3;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int tid = threadIdx.x;
+  float* prm = lds + WIDE_L_PRM;
+  float* scr = lds + WIDE_L_SCR + wave * RES_SCR;
+  float* cp = lds + WIDE_L_RED;
+  float* misc = lds + WIDE_L_MISC;
+  for (int i = tid; i < npt; i += RES_NW * 64) prm[i] = a.params[i];
+  if (tid == 0) a.flags[1] = 0;
+  LD e0, eo;
+  wide_desc<KS, FB, HA>(lt, e0, eo);
+  __syncthreads();
+  WideState<KS, FB> S;
+  for (int s = 0; s < a.steps; ++s) {
+    const int64_t base = (int64_t)s * a.bs;
+    const int nb = (int)min((int64_t)a.bs, (int64_t)a.n - base);
+    wide_zero(S);
+    RowMap rm = {nullptr, a.perm, base, nb, 0, 1, true};
+    const uint64_t seed = a.seed_base + (uint64_t)(a.iter0 + 1 + s);
+    const float inv = 1.f / (float)(nb * 3);
+    const int nblk = (nb + RES_T - 1) / RES_T;
+    for (int blk = wave; blk < nblk; blk += RES_NW)
+      wide_block(S, e0, eo, prm, a.x, a.ytrue, rm, (int64_t)blk * RES_T, seed, inv, scr, g, c);
+    wide_reduce(S, e0, eo, cp, npt, stride, wave, g, c, lane);
+    res_opt_step<true>(a, prm, nullptr, nullptr, cp, stride, npt, s, misc, tid, lane, wave);
+  }
+  for (int i = tid; i < npt; i += RES_NW * 64) {
+    const float w = prm[i];
+    a.params[i] = w;
+    const int tp = a.tpos[i];
+    if (tp >= 0) a.params_t[tp] = w;
+  }
+}
+
 // ---- host side ----------------------------------------------------------------------------------
 typedef void (*res_train_fn)(Args);
 typedef void (*res_fit_fn)(ResFitArgs);
 
+#ifndef RES_FAST
+#define RES_FAST 0
+#endif
+#define RES_HA (RES_FAST ? ACT_SOFTSIGN : -1)
 #if RES_PART != 0
 template <int KS, bool BOTL>
 static void res_pick_nb(int nb, res_train_fn* t, res_fit_fn* f) {
   switch (nb) {
-    case 1: *t = res_train_kernel<KS, 1, BOTL>; *f = res_fit_kernel<KS, 1, BOTL>; break;
-    case 2: *t = res_train_kernel<KS, 2, BOTL>; *f = res_fit_kernel<KS, 2, BOTL>; break;
-    case 3: *t = res_train_kernel<KS, 3, BOTL>; *f = res_fit_kernel<KS, 3, BOTL>; break;
-    case 4: *t = res_train_kernel<KS, 4, BOTL>; *f = res_fit_kernel<KS, 4, BOTL>; break;
+    case 1: *t = res_train_kernel<KS, 1, BOTL, RES_HA>; *f = res_fit_kernel<KS, 1, BOTL, RES_HA>; break;
+    case 2: *t = res_train_kernel<KS, 2, BOTL, RES_HA>; *f = res_fit_kernel<KS, 2, BOTL, RES_HA>; break;
+    case 3: *t = res_train_kernel<KS, 3, BOTL, RES_HA>; *f = res_fit_kernel<KS, 3, BOTL, RES_HA>; break;
+    case 4: *t = res_train_kernel<KS, 4, BOTL, RES_HA>; *f = res_fit_kernel<KS, 4, BOTL, RES_HA>; break;
     default: break;
   }
 }
-#define RES_FNS_NAME2(n) res_fns_##n
-#define RES_FNS_NAME(n) RES_FNS_NAME2(n)
-void RES_FNS_NAME(RES_PART)(int nb, bool bot, res_train_fn* t, res_fit_fn* f) {
+#define RES_FNS_NAME3(n, f) res_fns_##n##_##f
+#define RES_FNS_NAME(n, f) RES_FNS_NAME3(n, f)
+// nb > 0: a residual stack of nb blocks (bot: with the bottleneck); nb = 0: the wide two-layer net
+// of hidden width 16 * fb
+void RES_FNS_NAME(RES_PART, RES_FAST)(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f) {
+  if (nb == 0) {
+    switch (fb) {
+      case 1: *t = wide_train_kernel<RES_PART / 4, 1, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 1, RES_HA>; break;
+      case 2: *t = wide_train_kernel<RES_PART / 4, 2, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 2, RES_HA>; break;
+      case 3: *t = wide_train_kernel<RES_PART / 4, 3, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 3, RES_HA>; break;
+      case 4: *t = wide_train_kernel<RES_PART / 4, 4, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 4, RES_HA>; break;
+      default: break;
+    }
+    return;
+  }
   if (bot) res_pick_nb<RES_PART / 4, true>(nb, t, f);
   else res_pick_nb<RES_PART / 4, false>(nb, t, f);
 }
 #else
-void res_fns_88(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
-void res_fns_96(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
+void res_fns_88_0(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
+void res_fns_88_1(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
+void res_fns_96_0(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
+void res_fns_96_1(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
+
+// the compile-time-activation kernels: every hidden dense softsign, the post-add activation relu,
+// the output linear (create_model_complex, Model-88/attention_model.py:97-169)
+static bool res_fast(const int* w) {
+  const int* o = w + w[H_OPS_OFF];
+  const int* lt = w + o[O_AUX0];
+  const int L = o[O_AUX1], cin = o[O_K], nb = o[O_AUX3], bot = o[O_FLAGS], F = o[O_N];
+  if (nb == 0) {   // wide two-layer net: W0 [C_in][F], b0, W1 [F][3], b1; softsign, linear
+    const int* e0 = lt;
+    const int* e1 = lt + RL_WORDS;
+    return L == 2 && e0[RL_W] == 0 && e0[RL_B] == cin * F && e1[RL_W] == cin * F + F && e1[RL_B] == cin * F + F + 3 * F &&
+           e0[RL_K] == cin && e0[RL_N] == F && e1[RL_K] == F && e1[RL_N] == 3 && e0[RL_ACT] == ACT_SOFTSIGN &&
+           e1[RL_ACT] == ACT_LINEAR && w[H_NPARAMS_TRAIN] == cin * F + F + 3 * F + 3;
+  }
+  if (o[O_MODE] != ACT_RELU || (bot != 0 && bot != 8)) return false;
+  int off = 0;
+  for (int l = 0; l < L; ++l) {
+    const int* e = lt + l * RL_WORDS;
+    const int K = l == 0 ? cin : (l == L - 1 ? (bot ? 8 : 16) : 16);
+    const int N = l == L - 1 ? 3 : ((bot && l == 2 * nb + 1) ? 8 : 16);
+    if (e[RL_K] != K || e[RL_N] != N || e[RL_W] != off || e[RL_B] != off + K * N) return false;
+    if (e[RL_ACT] != (l == L - 1 ? ACT_LINEAR : ACT_SOFTSIGN)) return false;
+    off += K * N + N;
+  }
+  return off == w[H_NPARAMS_TRAIN];
+}
 
 static bool res_pick(const int* w, res_train_fn* t, res_fit_fn* f) {
   *t = nullptr;
   *f = nullptr;
   const int* o = w + w[H_OPS_OFF];
-  if (o[O_TYPE] != OP_RES || o[O_N] != 16) return false;
-  const int cin = o[O_K], nb = o[O_AUX3];
+  if (o[O_TYPE] != OP_RES) return false;
+  const int cin = o[O_K], nb = o[O_AUX3], F = o[O_N];
   const bool bot = o[O_FLAGS] > 0;
-  if (o[O_AUX1] != 2 * nb + 2 + (bot ? 1 : 0)) return false;
-  if (cin == 88) res_fns_88(nb, bot, t, f);
-  else if (cin == 96) res_fns_96(nb, bot, t, f);
+  if (nb > 0 && (F != 16 || o[O_AUX1] != 2 * nb + 2 + (bot ? 1 : 0))) return false;
+  if (nb == 0 && (F % 16 || F < 16 || F > 64 || bot || o[O_AUX1] != 2)) return false;
+  const bool fast = res_fast(w);
+  if (cin == 88) (fast ? res_fns_88_1 : res_fns_88_0)(nb, bot, F / 16, t, f);
+  else if (cin == 96) (fast ? res_fns_96_1 : res_fns_96_0)(nb, bot, F / 16, t, f);
   return *t != nullptr;
 }
 int res_supported(const int* w) {
   res_train_fn t;
   res_fit_fn f;
-  return w[H_MODE] == MODE_TRAIN && w[H_NPARAMS_TRAIN] <= RES_MAXP && res_pick(w, &t, &f) ? 1 : 0;
+  const int* o = w + w[H_OPS_OFF];
+  const int maxp = o[O_TYPE] == OP_RES && o[O_AUX3] == 0 ? WIDE_MAXP : RES_MAXP;
+  return w[H_MODE] == MODE_TRAIN && w[H_NPARAMS_TRAIN] <= maxp && res_pick(w, &t, &f) ? 1 : 0;
 }
 
 int res_grid_cap(int n_cu) { return n_cu; }
@@ -638,9 +1029,10 @@ int res_launch(const int* w, const Args& a, int grid, hipStream_t s) {
   res_train_fn t;
   res_fit_fn f;
   if (!res_pick(w, &t, &f)) return 2;
-  hipFuncSetAttribute((const void*)t, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_BYTES);
+  const int lds = w[w[H_OPS_OFF] + O_AUX3] == 0 ? WIDE_LDS_BYTES : RES_LDS_BYTES;
+  hipFuncSetAttribute((const void*)t, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   hpe_tev_begin(s);
-  hipLaunchKernelGGL(t, dim3(grid), dim3(RES_NW * 64), RES_LDS_BYTES, s, a);
+  hipLaunchKernelGGL(t, dim3(grid), dim3(RES_NW * 64), lds, s, a);
   hpe_tev_end(s);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
@@ -662,9 +1054,10 @@ int res_fit_launch(const int* w, const int* dwords, float* params, float* params
   a.alpha = alpha; a.seed_base = seed_base; a.iter0 = iter0;
   a.stats = stats; a.stats_stride = stats_stride;
   a.flags = (int*)workspace;
-  hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_BYTES);
+  const int lds = w[w[H_OPS_OFF] + O_AUX3] == 0 ? WIDE_LDS_BYTES : RES_LDS_BYTES;
+  hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   hpe_tev_begin(s);
-  hipLaunchKernelGGL(f, dim3(1), dim3(RES_NW * 64), RES_LDS_BYTES, s, a);
+  hipLaunchKernelGGL(f, dim3(1), dim3(RES_NW * 64), lds, s, a);
   hpe_tev_end(s);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -1336,6 +1336,21 @@ extern "C" int hpe_forward(const hpe_program* p, const float* params, const floa
   return launch(p, a, a.nrows, (hipStream_t)stream);
 }
 
+extern "C" int hpe_train_step_bounded(const hpe_program* p, const float* params, const float* params_t,
+                                      const float* x, const float* ytrue, int64_t n_images, int32_t P,
+                                      const int32_t* idx, int64_t img_off, float inv_count, uint64_t seed,
+                                      float x_bound, void* ws, void* stream) {
+  if (!p || !params || !x || !ytrue || !ws) return fail(HPE_EINVAL, "hpe_train_step: null argument");
+  if (!(x_bound >= 0.f)) return fail(HPE_EINVAL, "hpe_train_step_bounded: bad bound");
+  if (p->hdr[H_MODE] == MODE_FWD) return fail(HPE_EINVAL, "hpe_train_step: program compiled for inference only");
+  if (n_images <= 0 || P <= 0) return fail(HPE_EINVAL, "hpe_train_step: bad shape n_images=%lld P=%d", (long long)n_images, P);
+  Args a = {};
+  a.prog = p->dwords; a.params = params; a.params_t = params_t ? params_t : params; a.x = x;
+  a.ytrue = ytrue; a.idx = idx; a.ws = (float*)ws; a.nrows = n_images * (int64_t)P; a.P = P;
+  a.img_off = img_off; a.inv_count = inv_count; a.seed = seed; a.x_bound = x_bound;
+  return launch(p, a, a.nrows, (hipStream_t)stream);
+}
+
 extern "C" int hpe_train_step(const hpe_program* p, const float* params, const float* params_t,
                               const float* x, const float* ytrue, int64_t n_images, int32_t P,
                               const int32_t* idx, int64_t img_off, float inv_count, uint64_t seed,

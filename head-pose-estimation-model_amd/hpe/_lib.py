@@ -19,6 +19,8 @@ SIGNATURES = {
     'hpe_forward': (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     'hpe_train_step': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _f, _u64,
                                       _vp, _vp]),
+    'hpe_train_step_bounded': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _f, _u64,
+                                              _f, _vp, _vp]),
     'hpe_reduce': (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp]),
     'hpe_optim_step': (ctypes.c_int, [_i32, _f, _f, _f, _f, _i64, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _i64, _vp, _vp]),
@@ -42,6 +44,8 @@ SIGNATURES = {
     'hpe_seg_mean': (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp]),
     'hpe_mha': (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
     'hpe_mha_xg': (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _vp]),
+    'hpe_attn_tail_supported': (ctypes.c_int, [_vp]),
+    'hpe_attn_tail': (ctypes.c_int, [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp]),
     'hpe_last_error': (ctypes.c_char_p, []),
     'hpe_build_id': (ctypes.c_char_p, []),
     'hpe_guard_peek': (ctypes.c_int, [_vp, _vp]),

@@ -24,7 +24,7 @@ from . import _lib
 BF_MAGIC = 0x46425048
 BFH_WORDS = 8
 (BFH_MAGIC, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF) = range(4)
-BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT = 1, 2, 3, 4
+BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT, BF_STAGE = 1, 2, 3, 4, 5
 # 8x8 maps and the detector heads: persistent direct-tap kernel (HPE_BF_DIRECT=0 -> tiles); the
 # 16x16 maps measured equal either way and keep the tile kernel
 import os as _os
@@ -40,6 +40,9 @@ def _direct(f, dw, cinp, nct, ks):
     f[BFO_CS], f[BFO_KS], f[BFO_NC], f[BFO_NCT], f[BFO_WAVES] = ks, ks, nct, nct, 4
     f[BFO_LDS] = 4 * (nct * 32 * ks + (10 * cinp if dw else 0))
 ROWS_PF = 4                 # float4 per thread the rows kernel prefetches per step (csrc RPF)
+# stage (csrc bf_stage_kernel): the blocks on maps of <= STAGE_MAX_HW positions and the detector
+# heads as one launch, one 8-wave workgroup per image, the map resident in LDS
+STAGE_MAX_HW, STAGE_NW, STAGE_PF, STAGE_MAXNC = 256, 8, 6, 3
 RES_NONE, RES_ID, RES_MAXPOOL = 0, 1, 2
 BUF_IMG, BUF_A, BUF_B, BUF_OUT0 = 0, 1, 2, 3
 (BFO_KIND, BFO_H, BFO_W, BFO_HO, BFO_WO, BFO_CIN, BFO_COUT, BFO_CINP, BFO_COUTP,
@@ -278,7 +281,69 @@ def _rows_plan(bl, cinp, nct, ks, cs):
     return None
 
 
-def build_plan(model_config, weights):
+def _stage_nc(nchunk, nct):
+    """csrc bfs_nc: fewest output-channel chunks per wave task with every task on its own wave."""
+    for nc in range(1, min(nct, STAGE_MAXNC) + 1):
+        if nct % nc == 0 and nchunk * (nct // nc) <= STAGE_NW:
+            return nc
+    return 0
+
+
+def _stage_record(recs):
+    """BF_STAGE record for the op records `recs` (blocks, each tap's heads right after it), or None
+    when they do not fit the stage kernel (map / channel geometry, LDS)."""
+    for k, f in enumerate(recs):
+        hw, wo, dw = f[BFO_HO] * f[BFO_WO], f[BFO_WO], f[BFO_DW]
+        if hw > STAGE_MAX_HW or hw % 32 or wo & (wo - 1) or f[BFO_NCT] > 4 or not _stage_nc(hw // 32, f[BFO_NCT]):
+            return None
+        if (f[BFO_COUTP] + (10 if dw else 0)) * (f[BFO_CINP] // 4) > STAGE_PF * STAGE_NW * 64:
+            return None
+        if k == 0 and not dw:
+            return None
+    blocks = [f for f in recs if f[BFO_DW]]
+    cs = max(f[BFO_COUTP] for f in blocks) + 4           # (cs / 4) odd: conflict-free b128 rows
+    mapf = max(f[BFO_HO] * f[BFO_WO] for f in blocks) * cs
+    wtf = max(f[BFO_COUTP] * f[BFO_KS] for f in recs)
+    dwf = max(10 * f[BFO_CINP] for f in blocks)
+    lds = 4 * (mapf + wtf + dwf)
+    if lds > 160 * 1024:
+        return None
+    f = [0] * BFO_WORDS
+    f[BFO_KIND], f[BFO_NI], f[BFO_CS], f[BFO_ROWS], f[BFO_COLS] = BF_STAGE, len(recs), cs, mapf, wtf
+    f[BFO_LDS], f[BFO_WAVES] = lds, STAGE_NW
+    return f
+
+
+def _with_stage(stem_op, block_ops, head_ops):
+    """Op list with the longest stage-able suffix of the blocks (and every detector head, placed
+    right after the block that produces its tap) behind one BF_STAGE record; the per-op list when
+    no suffix qualifies."""
+    heads_of = {}
+    for f in head_ops:
+        heads_of.setdefault(f[BFO_SRC], []).append(f)
+    for b0 in range(len(block_ops)):
+        suffix = block_ops[b0:]
+        if any(f[BFO_HO] * f[BFO_WO] > STAGE_MAX_HW for f in suffix):
+            continue
+        recs, placed = [], 0
+        for f in suffix:
+            recs.append(f)
+            for h in heads_of.get(f[BFO_DST], []) if f[BFO_DST] >= BUF_OUT0 else []:
+                recs.append(h)
+                placed += 1
+        if placed != len(head_ops) or len(recs) > 16:
+            continue
+        rec = _stage_record(recs)
+        if rec is not None:
+            return [stem_op] + block_ops[:b0] + [rec] + recs
+    return [stem_op] + block_ops + head_ops
+
+
+def build_plan(model_config, weights, stage=None):
+    """Plan words + packed parameters.  stage: run the small-map blocks and the heads as one
+    bf_stage_kernel launch (default: env HPE_BF_STAGE, on)."""
+    if stage is None:
+        stage = _os.environ.get('HPE_BF_STAGE', '1') != '0'
     st = parse(model_config)
     P = _Params()
     ops = []
@@ -410,6 +475,8 @@ def build_plan(model_config, weights):
         if USE_DIRECT:
             _direct(f, False, cinp, nct, ks)
         ops.append(f)
+    if stage:
+        ops = _with_stage(ops[0], ops[1:1 + len(st['blocks'])], ops[1 + len(st['blocks']):])
     hdr = [0] * BFH_WORDS
     hdr[BFH_MAGIC], hdr[BFH_NOPS], hdr[BFH_ACT_FLOATS], hdr[BFH_OPS_OFF] = BF_MAGIC, len(ops), act_floats, BFH_WORDS
     words = np.asarray(hdr + [x for f in ops for x in f], dtype=np.int64)
@@ -430,12 +497,12 @@ class BlazeFace:
     """Batched forward of the unified BlazeFace + regressor graph.  ``predict(images)`` returns
     the unified model's outputs (Keras order) as numpy arrays; ``forward`` keeps them on device."""
 
-    def __init__(self, model_config, weights, device=None):
+    def __init__(self, model_config, weights, device=None, stage=None):
         if not torch.cuda.is_available():
             raise _lib.HPEError('hpe needs a ROCm GPU (MI355X / gfx950); torch.cuda is unavailable')
         from .engine import Engine
         self.device = torch.device(device or 'cuda')
-        self.plan = build_plan(model_config, weights)
+        self.plan = build_plan(model_config, weights, stage=stage)
         st = self.plan['structure']
         lib = _lib.load()
         h = ctypes.c_void_p()
@@ -516,15 +583,21 @@ class BlazeFace:
 
 def work_per_image(plan):
     """Algorithmic work of one 128x128 frame through the plan: FLOP = 2*MAC of the
-    convs (depthwise, pointwise, stem, heads) and the regressors; bytes = each fused op's compulsory
-    HBM traffic (its input map + its output map, fp32, padded channel strides as stored) plus the
-    regressors' tap reads and pose writes."""
+    convs (depthwise, pointwise, stem, heads) and the regressors; bytes = each launch's compulsory
+    HBM traffic (a per-op kernel: its input map + its output map, fp32, padded channel strides as
+    stored; the stage: its input map, the taps and the head outputs) plus the regressors' tap reads
+    and pose writes."""
     words = plan['words']
     flop = 0
     nbytes = 0
     off = int(words[BFH_OPS_OFF])
+    staged = 0          # records left in the current stage: their maps stay in LDS
     for i in range(int(words[BFH_NOPS])):
         f = [int(v) for v in words[off + i * BFO_WORDS: off + (i + 1) * BFO_WORDS]]
+        if f[BFO_KIND] == BF_STAGE:
+            staged = f[BFO_NI]
+            first = True
+            continue
         hw_in, hw_out = f[BFO_H] * f[BFO_W], f[BFO_HO] * f[BFO_WO]
         if f[BFO_KIND] == BF_STEM:
             flop += 2 * hw_out * 25 * 3 * f[BFO_COUT]
@@ -534,6 +607,13 @@ def work_per_image(plan):
             flop += 2 * hw_out * 9 * f[BFO_CIN]
         flop += 2 * hw_out * f[BFO_CIN] * f[BFO_COUT]
         out_c = f[BFO_COUT] if f[BFO_SPLIT] else f[BFO_OSTRIDE]
+        if staged:
+            # inside a stage only the stage input, the taps and the head outputs touch HBM
+            nbytes += 4 * (hw_in * f[BFO_CINP] if first else 0)
+            nbytes += 4 * hw_out * out_c if f[BFO_DST] >= BUF_OUT0 else 0
+            staged -= 1
+            first = False
+            continue
         nbytes += 4 * (hw_in * f[BFO_CINP] + hw_out * out_c)
     st = plan['structure']
     for r in st['regressors']:

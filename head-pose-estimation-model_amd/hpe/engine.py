@@ -164,20 +164,23 @@ class Engine:
     # reduction to the optimizer launch (hpe_reduce_optim_step: one launch fewer per step)
     FUSED_REDUCE_MAX_GRID = 16
 
-    def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0, defer_reduce=False):
+    def gradient(self, x, y, P, idx, n_images, inv_count, seed, img_off=0, defer_reduce=False, x_bound=0.0):
         """fwd + loss + bwd over this rank's images; self.grad = [dL/dparams..., sse, sae, 0, 0].
         defer_reduce: a single-rank fit step whose next call is optimizer_step may leave the
         per-workgroup slabs unreduced; optimizer_step then reduces and updates in one launch
-        (self.grad is written by that launch, bit-identical to hpe_reduce's)."""
+        (self.grad is written by that launch, bit-identical to hpe_reduce's).  x_bound: a known
+        bound on max |x| (fit: once per call over the resident dataset; 0 = unknown) that lets the
+        fp16-split kernels skip their exact-fp32 twin launch (hpe_train_step_bounded)."""
         if P > 1 and self.spatial() is not None:
             raise ValueError('fit of attention heads runs on 1x1 maps (train_88.py:270-305)')
         c = self.program('train', P)
         lib = _lib.load()
         rows = n_images * P
         ws = c.workspace(rows, self.device)
-        _lib.check(lib.hpe_train_step(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), _ptr(y),
-                                      n_images, P, _ptr(idx), img_off, float(inv_count),
-                                      int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(ws), _stream()),
+        _lib.check(lib.hpe_train_step_bounded(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(x), _ptr(y),
+                                              n_images, P, _ptr(idx), img_off, float(inv_count),
+                                              int(seed) & 0xFFFFFFFFFFFFFFFF, float(x_bound), _ptr(ws),
+                                              _stream()),
                    'hpe_train_step')
         self._pending = None
         if defer_reduce and lib.hpe_launch_grid(c.h, rows) <= self.FUSED_REDUCE_MAX_GRID:

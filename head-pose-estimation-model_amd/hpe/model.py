@@ -261,6 +261,11 @@ class Model:
         # launch (csrc/hpe_fit.hip); otherwise one train_step + reduce + optimizer per step
         fused = eng.fit_epoch_supported(bs, P, world)
         self._last_fit_fused = fused
+        # one bound on the resident rows per call: below the fp16 split's data range (64) the
+        # per-step launches skip their exact-fp32 twin (csrc/hpe_mlp2.hip launch_pair)
+        x_bound = 0.0 if fused else float(xd.abs().max().item()) if xd.numel() else 0.0
+        if not np.isfinite(x_bound):
+            x_bound = 0.0
         if fused:  # [sse, sae, per-wave regularisation shares of the 4 G waves]
             stats = torch.zeros((steps, 2 + 4 * eng.fit_groups()), dtype=torch.float32, device=eng.device)
         for epoch in range(initial_epoch, epochs):
@@ -282,7 +287,7 @@ class Model:
                 seed = hrandom.dropout_seed(eng.iterations + 1)
                 if r1 > r0:
                     eng.gradient(xd, yd, P, idx[r0:r1], r1 - r0, 1.0 / (nb * P * 3), seed,
-                                 img_off=r0 - b0, defer_reduce=world == 1)
+                                 img_off=r0 - b0, defer_reduce=world == 1, x_bound=x_bound)
                 else:
                     eng.grad.zero_()
                 if world > 1:

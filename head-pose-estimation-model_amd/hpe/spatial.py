@@ -239,6 +239,116 @@ class SpatialPlan:
         out = remap.get(out, out)
         self.head_config = _model('spatial_head', sub_layers, sub_in, out)
         self.head_weights = sub_w
+        self.tail = None
+        if self.mha is not None and len(res_add) == 1 and not readers:
+            self.tail = _attn_tail(sub_layers, sub_w, C, self.mha['H'] * self.mha['D'], out)
+
+
+# csrc/hpe_tail.hip descriptor words
+(TD_C, TD_HD, TD_FF, TD_HID, TD_ACT_FF, TD_ACT_HID, TD_ACT_OUT, TD_EPS1, TD_EPS2, TD_NW,
+ TD_BO, TD_G1, TD_BE1, TD_BF1, TD_BF2, TD_G2, TD_BE2, TD_BC1, TD_BC2) = range(19)
+TD_WORDS = 20
+
+
+def _mfma_order(w, K, N):
+    """[K][N] kernel -> the attention-tail kernel's LDS order [K/16][N/16][g][c][s] =
+    W[16 bk + 4 g + s][16 bn + c] (zero padded to 16-multiples)."""
+    kb, nb = -(-K // 16), -(-N // 16)
+    p = np.zeros((kb * 16, nb * 16), np.float32)
+    p[:K, :N] = np.asarray(w, np.float32).reshape(K, N)
+    return p.reshape(kb, 4, 4, nb, 16).transpose(0, 3, 1, 4, 2).ravel()
+
+
+def _attn_tail(layers, w, C, HD, out):
+    """Recognise program D of se_transformer_regr_head (Model-88/attention_model.py:56-72): the
+    [I; Wo] Dense of the residual Add, LayerNorm, Dense(ff) -> Dense(C), Add, LayerNorm, 1x1 conv
+    (hidden) -> 1x1 conv (3), and prepare it for csrc/hpe_tail.hip (weights in MFMA order, padded
+    vectors, descriptor); None when the graph is anything else."""
+    by = {l['name']: l for l in layers}
+    ins = {l['name']: [i[0] for i in l['inbound_nodes'][0]] if l['inbound_nodes'] else [] for l in layers}
+    cons = {}
+    for n, ii in ins.items():
+        for i in ii:
+            cons.setdefault(i, []).append(n)
+
+    def one(n, cls):
+        nx = cons.get(n, [])
+        if len(nx) != 1 or by[nx[0]]['class_name'] != cls:
+            return None
+        return nx[0]
+    try:
+        seq = [l['name'] for l in layers]
+        d0 = seq[1]
+        if by[d0]['class_name'] != 'Dense' or by[d0]['config'].get('activation', 'linear') != 'linear':
+            return None
+        ln1 = one(d0, 'LayerNormalization')
+        f1 = [n for n in cons.get(ln1, []) if by[n]['class_name'] == 'Dense']
+        add = [n for n in cons.get(ln1, []) if by[n]['class_name'] == 'Add']
+        if len(cons.get(ln1, [])) != 2 or len(f1) != 1 or len(add) != 1:
+            return None
+        f1 = f1[0]
+        f2 = one(f1, 'Dense')
+        if one(f2, 'Add') != add[0] or sorted(ins[add[0]]) != sorted([ln1, f2]):
+            return None
+        ln2 = one(add[0], 'LayerNormalization')
+        c1 = one(ln2, 'Conv2D')
+        c2 = one(c1, 'Conv2D')
+        if c2 != out or cons.get(c2):
+            return None
+    except KeyError:
+        return None
+    for n in (add[0],):
+        if by[n]['config'].get('activation', 'linear') not in (None, 'linear'):
+            return None
+    for n in (c1, c2):
+        cfg = by[n]['config']
+        if tuple(cfg.get('kernel_size', (1, 1))) != (1, 1) or tuple(cfg.get('strides', (1, 1))) != (1, 1):
+            return None
+
+    def kern(n, K):
+        k = np.asarray(w[n + '/kernel'], np.float32)
+        return k.reshape(K, -1)
+
+    def vec(n, key, size, fill=0.0):
+        k = n + '/' + key
+        return np.asarray(w[k], np.float32).ravel() if k in w else np.full(size, fill, np.float32)
+    FF = int(by[f1]['config']['units'])
+    HID = int(by[c1]['config']['filters'])
+    if int(by[f2]['config']['units']) != C or int(by[c2]['config']['filters']) != 3:
+        return None
+    wo = kern(d0, C + HD)[C:]                    # [I; Wo]: the identity rows are the residual xg
+    if not np.array_equal(kern(d0, C + HD)[:C], np.eye(C, dtype=np.float32)):
+        return None
+    parts = [_mfma_order(wo, HD, C), _mfma_order(kern(f1, C), C, FF), _mfma_order(kern(f2, FF), FF, C),
+             _mfma_order(kern(c1, C), C, HID), _mfma_order(kern(c2, HID), HID, 3)]
+
+    def pad(v, n):
+        out = np.zeros(-(-n // 16) * 16, np.float32)
+        out[:v.size] = v
+        return out
+
+    def ln_vec(n, key, fill):
+        cfg = by[n]['config']
+        on = cfg.get('scale', True) if key == 'gamma' else cfg.get('center', True)
+        return vec(n, key, C, fill) if on else np.full(C, fill, np.float32)
+    vecs = [('bo', vec(d0, 'bias', C), C), ('g1', ln_vec(ln1, 'gamma', 1.0), C), ('be1', ln_vec(ln1, 'beta', 0.0), C),
+            ('bf1', vec(f1, 'bias', FF), FF), ('bf2', vec(f2, 'bias', C), C), ('g2', ln_vec(ln2, 'gamma', 1.0), C),
+            ('be2', ln_vec(ln2, 'beta', 0.0), C), ('bc1', vec(c1, 'bias', HID), HID), ('bc2', vec(c2, 'bias', 3), 3)]
+    d = np.zeros(TD_WORDS, np.int64)
+    off = sum(p.size for p in parts)
+    for i, (_, v, n) in enumerate(vecs):
+        d[TD_BO + i] = off
+        parts.append(pad(v, n))
+        off += parts[-1].size
+    buf = np.concatenate(parts).astype(np.float32)
+    d[TD_C], d[TD_HD], d[TD_FF], d[TD_HID] = C, HD, FF, HID
+    d[TD_ACT_FF] = ACTS[by[f1]['config'].get('activation', 'linear')]
+    d[TD_ACT_HID] = ACTS[by[c1]['config'].get('activation', 'linear')]
+    d[TD_ACT_OUT] = ACTS[by[c2]['config'].get('activation', 'linear')]
+    d[TD_EPS1] = np.float32(by[ln1]['config'].get('epsilon', 1e-3)).view(np.int32)
+    d[TD_EPS2] = np.float32(by[ln2]['config'].get('epsilon', 1e-3)).view(np.int32)
+    d[TD_NW] = buf.size
+    return {'desc': d.astype(np.int32), 'w': buf, 'FF': FF, 'HID': HID}
 
 
 class SpatialHead:
@@ -258,6 +368,15 @@ class SpatialHead:
                        for k, v in pl.se.items()}
         self.qkv = Engine(pl.qkv_config, pl.qkv_weights, device=device) if pl.mha else None
         self.head = Engine(pl.head_config, pl.head_weights, device=device)
+        # the post-attention tail of se_transformer_regr_head in one kernel (csrc/hpe_tail.hip);
+        # HPE_ATTN_TAIL=0 keeps the row program D
+        self.tail = None
+        import os
+        if pl.tail is not None and os.environ.get('HPE_ATTN_TAIL', '1') != '0':
+            import ctypes
+            desc = (ctypes.c_int32 * TD_WORDS)(*[int(v) for v in pl.tail['desc']])
+            if _lib.load().hpe_attn_tail_supported(desc) == 1:
+                self.tail = {'desc': desc, 'w': torch.from_numpy(pl.tail['w']).to(device)}
 
     def forward(self, x, P, out=None):
         """x: device fp32 [n_images * P, C] rows -> [n_images * P, C_out]."""
@@ -284,6 +403,15 @@ class SpatialHead:
             return self.head.forward(xg, P, out=out)
         H, D = pl.mha['H'], pl.mha['D']
         qkv = self.qkv.forward(xg, P)
+        if self.tail is not None:
+            # attention core writes o alone (no pass-through columns); the tail reads xg and o
+            o = torch.empty((x.shape[0], H * D), dtype=torch.float32, device=x.device)
+            _lib.check(lib.hpe_mha_xg(_ptr(qkv), qkv.shape[1], _ptr(None), 0, _ptr(o), H * D, n, P, H, D, _stream()),
+                       'hpe_mha_xg')
+            y = out if out is not None else torch.empty((x.shape[0], 3), dtype=torch.float32, device=x.device)
+            _lib.check(lib.hpe_attn_tail(_ptr(xg), self.C, _ptr(o), H * D, x.shape[0], self.tail['desc'],
+                                         _ptr(self.tail['w']), _ptr(y), _stream()), 'hpe_attn_tail')
+            return y
         xo = torch.empty((x.shape[0], self.C + H * D), dtype=torch.float32, device=x.device)
         _lib.check(lib.hpe_mha_xg(_ptr(qkv), qkv.shape[1], _ptr(xg), self.C, _ptr(xo), xo.shape[1], n, P, H, D,
                                   _stream()), 'hpe_mha_xg')

@@ -73,6 +73,15 @@ int hpe_train_step(const hpe_program *prog, const float *params, const float *pa
                    const int32_t *image_index, int64_t image_offset, float inv_count,
                    uint64_t dropout_seed, void *workspace, void *stream);
 
+/* hpe_train_step with the caller's bound on max |x| over the rows the launch reads (0 = unknown).
+ * The fused kernels compute the GEMMs on an fp16 split whose data side holds |x| < 64 and hand a launch
+ * whose split overflowed to an exact-fp32 twin launched behind it; with x_bound in (0, 64) the twin
+ * cannot be needed and is not launched (fit bounds its resident dataset once per call). */
+int hpe_train_step_bounded(const hpe_program *prog, const float *params, const float *params_t,
+                           const float *x, const float *y_true, int64_t n_images, int32_t P,
+                           const int32_t *image_index, int64_t image_offset, float inv_count,
+                           uint64_t dropout_seed, float x_bound, void *workspace, void *stream);
+
 /* grad[i] = sum over workgroups of workspace partials, i < n_params + 4 (fixed order). */
 int hpe_reduce(const hpe_program *prog, int64_t n_rows, const void *workspace, float *grad,
                void *stream);
@@ -228,6 +237,18 @@ int hpe_mha(const float *in, int32_t ld_in, int32_t C, float *out, int32_t ld_ou
  * identity block for xg: 2 * C * C fewer FLOPs and C fewer stored floats per row). */
 int hpe_mha_xg(const float *qkv, int32_t ld_qkv, const float *xg, int32_t C, float *out, int32_t ld_out,
                int64_t n_images, int32_t P, int32_t H, int32_t D, void *stream);
+
+/* hpe_attn_tail: the row-local tail of se_transformer_regr_head after the attention core
+ * (Model-88/attention_model.py:56-72: residual Add of the attention output, LayerNorm, feed-forward
+ * Dense -> Dense, residual Add, LayerNorm, 1x1 conv hidden -> 1x1 conv 3) in one kernel: reads xg
+ * [n_rows][ld_xg >= C] and the attention output o [n_rows][ld_o >= H*D] (hpe_mha_xg with C = 0),
+ * writes y [n_rows][3].  desc: 20 host int32 words (C, H*D, ff_dim, hidden, activations, the two
+ * LayerNorm epsilons as float bits, the parameter buffer's size and vector offsets); w: the device
+ * parameter buffer hpe/spatial.py:_attn_tail prepares (weights in MFMA operand order, padded
+ * vectors).  hpe_attn_tail_supported(desc): 1 when a kernel is compiled for these widths. */
+int hpe_attn_tail_supported(const int32_t *desc);
+int hpe_attn_tail(const float *xg, int32_t ld_xg, const float *o, int32_t ld_o, int64_t n_rows,
+                  const int32_t *desc, const float *w, float *y, void *stream);
 
 #ifdef __cplusplus
 }

@@ -7,10 +7,11 @@ CS=$ROOT/head-pose-estimation-model_amd/csrc
 make -C $CS -j8 >/dev/null
 mkdir -p $ROOT/varlibs $CS/build_var
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -mllvm -amdgpu-use-amdgpu-trackers=1 -DRES_STAMPS $*"
-/opt/rocm/bin/hipcc $F -DRES_PART=88 -c -o $CS/build_var/res88_st.o $CS/hpe_res.hip &
-/opt/rocm/bin/hipcc $F -DRES_PART=96 -c -o $CS/build_var/res96_st.o $CS/hpe_res.hip &
+for p in 88 96; do for f in 0 1; do
+  /opt/rocm/bin/hipcc $F -DRES_PART=$p -DRES_FAST=$f -c -o $CS/build_var/res${p}_${f}_st.o $CS/hpe_res.hip &
+done; done
 /opt/rocm/bin/hipcc $F -c -o $CS/build_var/res0_st.o $CS/hpe_res.hip &
 wait
 objs=$(ls $CS/build/*.o | grep -v hpe_res)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/varlibs/libhpe_rst.so $objs $CS/build_var/res88_st.o $CS/build_var/res96_st.o $CS/build_var/res0_st.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/varlibs/libhpe_rst.so $objs $CS/build_var/res*_st.o
 echo built varlibs/libhpe_rst.so

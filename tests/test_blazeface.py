@@ -96,6 +96,80 @@ def test_capi_validates_plan_without_gpu():
     assert lib.hpe_blazeface_create(bad.ctypes.data_as(ctypes.c_void_p), bad.size, ctypes.byref(h)) == 1
 
 
+def _records(words):
+    off = int(words[B.BFH_OPS_OFF])
+    return [[int(v) for v in words[off + i * B.BFO_WORDS: off + (i + 1) * B.BFO_WORDS]]
+            for i in range(int(words[B.BFH_NOPS]))]
+
+
+@pytest.mark.parametrize('rid', UNIFIED)
+def test_stage_plan_covers_small_maps_and_heads(rid):
+    """The plan's one BF_STAGE record covers every block from the 32x32 -> 16x16 stride-2 block on,
+    each tap's two detector heads right after the block producing the tap; the per-op plan
+    (stage=False) holds the same records in block-then-heads order."""
+    mc, w = fixture(rid)
+    recs = _records(B.build_plan(mc, w)['words'])
+    per_op = _records(B.build_plan(mc, w, stage=False)['words'])
+    k = [i for i, f in enumerate(recs) if f[B.BFO_KIND] == B.BF_STAGE]
+    assert len(k) == 1
+    st = recs[k[0]]
+    covered = recs[k[0] + 1:k[0] + 1 + st[B.BFO_NI]]
+    assert k[0] + 1 + st[B.BFO_NI] == len(recs)
+    assert covered[0][B.BFO_HO] == 16 and covered[0][B.BFO_H] == 32 and covered[0][B.BFO_STRIDE] == 2
+    assert all(f[B.BFO_HO] * f[B.BFO_WO] <= 256 for f in covered)
+    assert sorted(map(tuple, covered)) == sorted(map(tuple, per_op[k[0]:]))
+    for i, f in enumerate(covered):
+        if not f[B.BFO_DW]:                       # heads read the tap the block before wrote
+            prev = [g for g in covered[:i] if g[B.BFO_DW]][-1]
+            assert f[B.BFO_SRC] == prev[B.BFO_DST] >= B.BUF_OUT0
+    assert st[B.BFO_LDS] <= 160 * 1024
+    assert B.work_per_image({'words': B.build_plan(mc, w)['words'], 'structure': B.parse(mc)})[0] == \
+        B.work_per_image({'words': B.build_plan(mc, w, stage=False)['words'], 'structure': B.parse(mc)})[0]
+
+
+def test_capi_validates_stage_record():
+    mc, w = fixture(RID)
+    words = np.ascontiguousarray(B.build_plan(mc, w)['words'], np.int32)
+    recs = _records(words)
+    k = [i for i, f in enumerate(recs) if f[B.BFO_KIND] == B.BF_STAGE][0]
+    base = B.BFH_WORDS + k * B.BFO_WORDS
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.hpe_blazeface_create(words.ctypes.data_as(ctypes.c_void_p), words.size, ctypes.byref(h)) == 0
+    lib.hpe_blazeface_destroy(h)
+    for field, val in ((B.BFO_NI, 99), (B.BFO_NI, len(recs) - k), (B.BFO_LDS, 200_000), (B.BFO_CS, 64),
+                       (B.BFO_ROWS, 100)):
+        bad = words.copy()
+        bad[base + field] = val
+        assert lib.hpe_blazeface_create(bad.ctypes.data_as(ctypes.c_void_p), bad.size, ctypes.byref(h)) == 1, field
+    # the first 8x8 head moved before the block that writes its tap
+    bad = words.copy()
+    a, b = base + 12 * B.BFO_WORDS, base + 13 * B.BFO_WORDS
+    assert bad[b + B.BFO_DW] == 0
+    bad[a:b + B.BFO_WORDS] = np.concatenate([words[b:b + B.BFO_WORDS], words[a:b]])
+    assert lib.hpe_blazeface_create(bad.ctypes.data_as(ctypes.c_void_p), bad.size, ctypes.byref(h)) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('rid', [RID, UNIFIED[2]])
+def test_blazeface_stage_matches_per_op_bit_for_bit(rid):
+    """bf_stage_kernel runs the same arithmetic as the per-op kernels (depthwise bias + 9 taps in
+    order, fp16-split MFMA over ascending channel quads, bias, residual, ReLU): outputs and taps are
+    bit-identical, at a ragged batch of 37 frames."""
+    import torch
+    mc, w = fixture(rid)
+    x = torch.from_numpy(_images(37, seed=37)).cuda()
+    res = {}
+    for stage in (False, True):
+        bf = B.BlazeFace(mc, w, stage=stage)
+        outs = [o.cpu().numpy() for o in bf.forward(x)]
+        res[stage] = (outs, {t: v.cpu().numpy() for t, v in bf.taps.items()})
+    for o, a, b in zip(B.parse(mc)['outputs'], res[False][0], res[True][0]):
+        np.testing.assert_array_equal(a, b, err_msg=o)
+    for t in res[False][1]:
+        np.testing.assert_array_equal(res[False][1][t], res[True][1][t], err_msg=t)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('rid,n', [(RID, 1), (RID, 5), (RID, 33)] + [(u, 3) for u in UNIFIED[1:]])
 def test_blazeface_forward_matches_oracle(rid, n):

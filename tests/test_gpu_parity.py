@@ -65,7 +65,12 @@ TRAIN_CASES = [
     ('66kjr5zw', 'adam', 100, 2),     # 512-256-128 residual + dropout: 3 passes, slots in device scratch
     ('6togj6se', 'adamax', 77, 2),    # 11-layer residual tanh stack: slots in device scratch
     ('s25l3n04', 'adam', 128, 2),     # 512-256-256-... residual: 3 passes + device-scratch slots
-    ('rtomubjl', 'adam', 64, 2),      # 128-wide residual stack with Activation layers and dropout
+    # 128-wide residual relu stack with Activation layers and dropout.  Adamax: with round 4's
+    # dropout masks the float64 oracle's own trajectory is ill-conditioned at fp32 resolution under
+    # SGD lr 0.05 (a 1-ulp fp32 perturbation of the initial weights moves conv2d_7/kernel by up to
+    # 7e-4, 97 elements past the bar: a relu kink) and under Adam (barely-active units: m / sqrt(v)
+    # ~ sign(g) of a rounding-level gradient); under Adamax it moves < 1e-6
+    ('rtomubjl', 'adamax', 64, 2),
     ('rd93oeou', 'adam', 100, 2),     # 256-128-... residual tanh stack: device-scratch slots
     ('rkq8scme', 'sgd', 90, 2),       # residual stack ending 32-8-3
     ('rdsncwuy', 'adamax', 128, 2),   # 128-256-512-3 with dropout: 2 passes
@@ -291,6 +296,27 @@ def test_train_step_split_vs_exact_and_guard(rid, P):
     np.testing.assert_array_equal(go, go_exact)
 
 
+@pytest.mark.parametrize('rid,P,n', [('sqnu665j', 1, 128), ('stoqa9pt', 1, 500), ('sqnu665j', 64, 4)])
+def test_train_step_bounded_matches_unbounded(rid, P, n):
+    """hpe_train_step_bounded (fit's per-step launches: x_bound = max |x| of the resident rows,
+    below the fp16 split's data range) launches no exact-fp32 twin; the split kernel's result is
+    the same bits as the guarded launch's (the twin exits without writing when the guard is clear)."""
+    from hpe.engine import Engine
+    mc, w = fixture(rid)
+    c = input_channels(mc)
+    eng = Engine(mc, w)
+    side = int(round(P ** 0.5))
+    x = features(n, c, seed=31, h=side, w=side)
+    y = labels(n, seed=32)
+    xt = torch.from_numpy(x.reshape(n * P, c)).cuda()
+    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
+    bound = float(np.abs(x).max())
+    assert 0 < bound < 64
+    g0 = eng.gradient(xt, yt, P, None, n, 1.0 / (n * P * 3), seed=3).cpu().numpy().copy()
+    g1 = eng.gradient(xt, yt, P, None, n, 1.0 / (n * P * 3), seed=3, x_bound=bound).cpu().numpy().copy()
+    np.testing.assert_array_equal(g0, g1)
+
+
 @pytest.mark.parametrize('F,act,dropout,side,n', [(360, 'tanh', 0.0, 96, 2), (360, 'tanh', 0.3, 8, 40),
                                                   (200, 'elu', 0.2, 6, 50), (256, 'relu', 0.1, 12, 20),
                                                   (137, 'softsign', 0.0, 33, 3)])
@@ -336,17 +362,16 @@ def test_train_step_8wave_kernel(F, act, dropout, side, n):
     np.testing.assert_allclose(g_split[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
 
 
-@pytest.mark.parametrize('rid,side,n,R', [('sqnu665j', 96, 2, 40), ('sqnu665j', 96, 24, 12),
+@pytest.mark.parametrize('rid,side,n,R', [('sqnu665j', 96, 2, 60), ('sqnu665j', 96, 24, 12),
                                           ('stoqa9pt', 88, 8, 24)])
 def test_train_step_repeatable(rid, side, n, R):
     """Race screen (scripts/diag_repeat.py as a test): the fused training step launched R times on
-    identical inputs.  sqnu665j at 96x96 runs mlp2v_kernel (n = 2: two or three tiles per
-    workgroup; n = 24: the steady-state X(t+2) staging pipeline), stoqa9pt at 88x88 the 4-wave
-    mlp2_kernel.  Bar: every run within 1e-6 of max |g| of the first (the split-vs-exact bar of
-    test_train_step_split_vs_exact_and_guard), so a lost partial sum (a missing LDS ordering) fails.
-    Bit-identical runs are the rule; mlp2v has shown rare runs (0-1 in 200-400 launches, DESIGN.md
-    'Open issue') that differ by <= 3e-7 of max |g|, the size of an exact-fp32 guard fallback — they
-    are printed, not failed."""
+    identical inputs must give bit-identical gradients.  sqnu665j at 96x96 runs mlp2v_kernel (n = 2:
+    two or three tiles per workgroup, the first tile's X(t+1) staged right before forward(0); n =
+    24: the steady-state X(t+2) staging), stoqa9pt at 88x88 the 4-wave mlp2_kernel.  Round 3 saw rare
+    runs (2 in ~3,700 launches) where one row's yaw head partial differed — traced to a wave's LDS-DMA
+    still in flight across that wave's head-partial LDS writes; with the DMA landed first
+    (hpe_mlp2.hip, vmcnt(0) before the partial writes) 0 of 9,960 launches differed."""
     from hpe.engine import Engine
     mc, w = fixture(rid)
     c = input_channels(mc)
@@ -359,16 +384,9 @@ def test_train_step_repeatable(rid, side, n, R):
     inv = 1.0 / (n * P * 3)
     ref = eng.gradient(xt, yt, P, None, n, inv, seed=5).cpu().numpy().copy()
     assert np.isfinite(ref).all()
-    scale = np.abs(ref).max()
-    worst, nbits = 0.0, 0
     for r in range(1, R):
         g = eng.gradient(xt, yt, P, None, n, inv, seed=5).cpu().numpy()
-        if not np.array_equal(g, ref):
-            nbits += 1
-            worst = max(worst, float(np.abs(g - ref).max() / scale))
-    print('%s %dx%d n=%d: %d of %d runs not bit-identical to run 0, max |diff| / max |g| = %.2e'
-          % (rid, side, side, n, nbits, R - 1, worst))
-    assert worst <= 1e-6, (nbits, worst)
+        assert np.array_equal(g, ref), 'run %d differs from run 0 in %d entries' % (r, int((g != ref).sum()))
 
 
 def _create_model(F, act, dropout, l2, lr=2.8e-4):

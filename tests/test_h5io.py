@@ -1,10 +1,14 @@
 """In-process Keras .h5 reader (hpe/h5io.py).
 
-Golden: four of the reference's own checkpoints, committed as data under tests/golden/h5/
-(Model-96 hrchr82r, Model-96 0g73t16n with its Adam state, Model-88 stoqa9pt with its SGD state,
-Model-88 ker7z9mv SE + MHA with Lambda layers), against the h5py conversions of the same files
-(tests/golden/models/*.json / .npz, tests/golden/make_fixtures.py).  When /root/reference is present
-(the build container) every one of its 688 .h5 files is parsed and each fixture exemplar compared.
+Golden: four of the reference's checkpoints, committed as data under tests/golden/h5/, against the
+h5py conversions of the same files (tests/golden/models/*.json / .npz, tests/golden/make_fixtures.py).
+Three are the files Keras wrote (Model-96 hrchr82r, Model-96 0g73t16n with its Adam state, Model-88
+stoqa9pt with its SGD state); the fourth, Model-88 ker7z9mv (SE + MHA with Lambda layers), was
+rewritten by this repo's own writer to drop the Lambda bytecode (tests/golden/strip_h5_bytecode.py).
+The Keras-written ker7z9mv is kept too, under tests/golden/h5_keras/, with only the Lambda bytecode
+overwritten in place by a same-length placeholder (tests/golden/patch_h5_lambda.py): every other
+byte is the file libhdf5 wrote.  When /root/reference is present (the build container) every one of
+its 688 .h5 files is parsed and each fixture exemplar compared.
 """
 import glob
 import json
@@ -17,6 +21,7 @@ from hpe import h5io
 from util import fixture
 
 H5 = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'h5')
+H5_KERAS = os.path.join(os.path.dirname(H5), 'h5_keras')
 MODELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'models')
 IDS = sorted(os.path.basename(p)[:-3] for p in glob.glob(os.path.join(H5, '*.h5')))
 
@@ -34,6 +39,23 @@ def test_reader_matches_h5py_conversion(rid):
     for k in ref_w:
         assert w[k].dtype == np.float32
         np.testing.assert_array_equal(w[k], ref_w[k], err_msg=k)
+
+
+def test_reader_on_keras_written_se_mha_lambda_file():
+    """The Keras-written SE + MHA + Lambda checkpoint (bytecode overwritten in place): the same
+    graph, weights and optimizer state as the h5py conversion and as the rewritten fixture."""
+    p = os.path.join(H5_KERAS, 'ker7z9mv.h5')
+    mc, w, opt = h5io.read_keras_h5(p, with_optimizer=True)
+    ref_mc, ref_w = fixture('ker7z9mv')
+    assert mc == ref_mc
+    assert sorted(w) == sorted(ref_w)
+    for k in ref_w:
+        np.testing.assert_array_equal(w[k], ref_w[k], err_msg=k)
+    _, _, opt2 = h5io.read_keras_h5(os.path.join(H5, 'ker7z9mv.h5'), with_optimizer=True)
+    assert list(opt) == list(opt2)
+    for k in opt:
+        np.testing.assert_array_equal(np.asarray(opt[k]), np.asarray(opt2[k]), err_msg=k)
+    assert h5io.read_training_config(p) == h5io.read_training_config(os.path.join(H5, 'ker7z9mv.h5'))
 
 
 @pytest.mark.parametrize('rid', ['0g73t16n', 'stoqa9pt'])
@@ -261,18 +283,21 @@ def test_no_reference_bytecode_in_committed_fixtures():
     sb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(sb)
     n_lambda = 0
-    for p in glob.glob(os.path.join(H5, '*.h5')):
+    for p in glob.glob(os.path.join(H5, '*.h5')) + glob.glob(os.path.join(H5_KERAS, '*.h5')):
         fns = sb.lambda_functions(sb.raw_model_config(p))
         n_lambda += len(fns)
-        assert all(f == '<bytecode stripped>' for f in fns), p
+        # our writer's plain placeholder, or Keras's [code, defaults, closure] with code patched
+        assert all(f == '<bytecode stripped>' or (isinstance(f, list) and f[0] == '<bytecode stripped>')
+                   for f in fns), p
     for p in glob.glob(os.path.join(MODELS, '*.json')):
         with open(p) as fh:
             d = json.load(fh)
         mc = d.get('model_config', d)
         if isinstance(mc, dict):
             assert all(f == '<bytecode stripped>' for f in sb.lambda_functions(mc)), p
-    assert n_lambda >= 2                     # ker7z9mv's reshape_flat / reshape_back
-    for p in glob.glob(os.path.join(H5, '*.h5')) + glob.glob(os.path.join(MODELS, '*.json')):
+    assert n_lambda >= 4                     # ker7z9mv's reshape_flat / reshape_back, both files
+    for p in (glob.glob(os.path.join(H5, '*.h5')) + glob.glob(os.path.join(H5_KERAS, '*.h5'))
+              + glob.glob(os.path.join(MODELS, '*.json'))):
         with open(p, 'rb') as fh:
             raw = fh.read()
         assert b'4wEAAAAA' not in raw and b'4wAAAAAA' not in raw, p

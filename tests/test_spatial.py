@@ -118,6 +118,71 @@ def test_staged_decomposition_matches_oracle(rid, hw):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
 
 
+def _tail_weights(tail, C, HD):
+    """Read the attention-tail buffer the way csrc/hpe_tail.hip does ([K/16][N/16][g][c][s] =
+    W[16 bk + 4 g + s][16 bn + c]) back into plain [K][N] kernels and the vectors."""
+    import hpe.spatial as S
+    d, buf = tail['desc'], tail['w']
+    FF, HID = int(d[S.TD_FF]), int(d[S.TD_HID])
+    shapes = [(HD, C), (C, FF), (FF, C), (C, HID), (HID, 3)]
+    out, off = [], 0
+    for K_, N_ in shapes:
+        kb, nb = -(-K_ // 16), -(-N_ // 16)
+        blk = buf[off:off + kb * nb * 256].reshape(kb, nb, 4, 16, 4).transpose(0, 2, 4, 1, 3)
+        out.append(blk.reshape(kb * 16, nb * 16)[:K_, :N_].astype(np.float64))
+        off += kb * nb * 256
+    assert off == int(d[S.TD_BO])
+    sizes = [C, C, C, FF, C, C, C, HID, 3]
+    vecs = [buf[int(d[S.TD_BO + i]):int(d[S.TD_BO + i]) + n].astype(np.float64) for i, n in enumerate(sizes)]
+    return out, vecs, d
+
+
+@pytest.mark.parametrize('rid', SPATIAL_IDS)
+def test_attn_tail_plan_matches_oracle(rid):
+    """The fused post-attention tail (csrc/hpe_tail.hip) as planned by hpe/spatial.py: its parameter
+    buffer, read back in the kernel's MFMA operand order and evaluated in float64 after the staged
+    SE gate / program B / attention core, reproduces the oracle's forward on 8x8 maps."""
+    mc, w = fixture(rid)
+    plan = SpatialPlan(mc, w)
+    if plan.mha is None:
+        pytest.skip('no attention core')
+    assert plan.tail is not None, 'se_transformer_regr_head tail not recognised'
+    c = plan.C
+    H, D = plan.mha['H'], plan.mha['D']
+    x = _inputs(2, 8, 8, c, seed=7)
+    P = 64
+    xr = x.reshape(-1, c).astype(np.float64)
+    n = 2
+    s = plan.se
+    m = xr.reshape(n, P, -1).mean(axis=1)
+    g = _act(s['act2'], _act(s['act1'], m @ s['w1'] + s['b1']) @ s['w2'] + s['b2'])
+    xg = (xr.reshape(n, P, -1) * g[:, None, :]).reshape(n * P, -1)
+    pb = C.compile_graph(plan.qkv_config, plan.qkv_weights, 'fwd', fused=False)
+    qkv = EMU.run(pb, _flat(pb, plan.qkv_weights), xg)['out']
+    q = qkv[:, :H * D].reshape(n, P, H, D)
+    k = qkv[:, H * D:2 * H * D].reshape(n, P, H, D)
+    v = qkv[:, 2 * H * D:].reshape(n, P, H, D)
+    sc = np.einsum('bthd,bshd->bhts', q, k)
+    a = np.exp(sc - sc.max(-1, keepdims=True))
+    a /= a.sum(-1, keepdims=True)
+    o = np.einsum('bhts,bshd->bthd', a, v).reshape(n * P, H * D)
+    (wo, wf1, wf2, wc1, wc2), (bo, g1, be1, bf1, bf2, g2, be2, bc1, bc2), d = _tail_weights(plan.tail, c, H * D)
+    import hpe.spatial as S
+
+    def ln(t, gm, bt, eps):
+        mu = t.mean(-1, keepdims=True)
+        var = ((t - mu) ** 2).mean(-1, keepdims=True)
+        return (t - mu) / np.sqrt(var + eps) * gm + bt
+    eps1 = float(np.int32(d[S.TD_EPS1]).view(np.float32))
+    eps2 = float(np.int32(d[S.TD_EPS2]).view(np.float32))
+    t = ln(xg + o @ wo + bo, g1, be1, eps1)
+    f = _act(int(d[S.TD_ACT_FF]), t @ wf1 + bf1) @ wf2 + bf2
+    z = ln(t + f, g2, be2, eps2)
+    y = _act(int(d[S.TD_ACT_OUT]), _act(int(d[S.TD_ACT_HID]), z @ wc1 + bc1) @ wc2 + bc2)
+    ref = K.Graph(mc, w).forward(x).detach().numpy().reshape(-1, 3)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
+
+
 def test_row_local_graph_is_not_spatial():
     mc, w = fixture('hrchr82r')
     assert not is_spatial(mc)
