@@ -606,6 +606,9 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     return;
   }
   // ---- flush this workgroup's partial gradients + loss sums ----
+#ifdef MLP2_DIAG_BAR_FLUSH
+  __syncthreads();
+#endif
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
@@ -1075,6 +1078,9 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
     return;
   }
   // ---- flush this workgroup's partial gradients + loss sums ----
+#ifdef MLP2_DIAG_BAR_FLUSH
+  __syncthreads();
+#endif
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
@@ -1338,8 +1344,12 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
   // dW2 / db1 partial sums per (lane group, unit) and wave 0's loss sums live in LDS, not in 17
   // loop-carried VGPRs (the kernel sits at its 256-register budget)
   float* gme = gacc + ((wave * 4 + lg) * 48 + lc) * 4;  // + 64 nb: this lane's (unit, group) slot
+#ifdef MLP2_DIAG_ZERO_LOOP
+  for (int i = threadIdx.x; i < V_NW * 4 * 48 * 4; i += V_NW * 64) gacc[i] = 0.f;
+#else
 #pragma unroll
   for (int nb = 0; nb < 3; ++nb) *(f32x4*)(gme + 64 * nb) = f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
   if (wave == 0 && half == 0) {
     *(f32x4*)(hac + l32 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
     *(f32x4*)(hac + l32 * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1499,9 +1509,11 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
     // ---- head(t): every wave, all 32 rows (lane r, halves take waves 0..3 / 4..7) ----
     {
       const int r = l32;
-      f32x4 sp = {0.f, 0.f, 0.f, 0.f};
+      // the four partials read before summing (one LDS round trip, not four), summed in wave order
+      f32x4 pu[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sp += *(const f32x4*)(pt + ((4 * half + u) * T + r) * 4);
+      for (int u = 0; u < 4; ++u) pu[u] = *(const f32x4*)(pt + ((4 * half + u) * T + r) * 4);
+      const f32x4 sp = ((pu[0] + pu[1]) + pu[2]) + pu[3];
       f32x4 ot;
       ot.x = xor32(sp.x);
       ot.y = xor32(sp.y);
@@ -1509,16 +1521,29 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
       ot.w = 0.f;
       const f32x4 zz = half ? ot + sp : sp + ot;  // (waves 0..3) + (waves 4..7) in every lane
       const int64_t R = row0 + r;
-      const int64_t img64 = ti.of(r) + args.img_off;
       const float* lab = lbuf + (it & 3) * MLP2_LAB;
       f32x4 gv = {0.f, 0.f, 0.f, 0.f};
       float esq = 0.f, eab = 0.f;
+      // the output SpatialDropout's keep bits only when it is on (uniform branch: the row's image
+      // and its hash are not computed every tile for the common no-dropout head); P >= 32 here, so
+      // a row's image is img0 or img0 + 1
+      const bool d2 = ACT1 < 0 || __builtin_expect(e2.drop >= 0, 0);
+      int64_t img64 = 0;
+      uint32_t k2 = 7u;
+      if (d2) {
+        img64 = ti.img0 + (ti.rem0 + r >= P ? 1 : 0) + args.img_off;
+        if (ACT1 >= 0) {
+          k2 = 0u;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) k2 |= drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr ? 1u << j : 0u;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const float z = zz[j] + b2t[j];
-        const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
-                                                         ? z / e2.keep : 0.f) : z)
-                                  : e_fwd(e2, args.seed, img64, j, z);
+        float p = z;
+        if (ACT1 < 0) p = e_fwd(e2, args.seed, img64, j, z);
+        else if (d2) p = (k2 >> j) & 1u ? z / e2.keep : 0.f;
         float g = 0.f;
         if (R < nrows) {
           const float err = p - lab[r * 4 + j];
@@ -1526,9 +1551,9 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
           eab += fabsf(err);
           g = 2.f * err;
         }
-        gv[j] = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
-                                                  ? g / e2.keep : 0.f) : g)
-                          : e_bwd(e2, args.seed, img64, j, g, p);
+        if (ACT1 < 0) g = e_bwd(e2, args.seed, img64, j, g, p);
+        else if (d2) g = (k2 >> j) & 1u ? g / e2.keep : 0.f;
+        gv[j] = g;
       }
       if (wave == 0 && half == 0) {
         f32x4 h0 = *(f32x4*)(hac + r * 8);
@@ -1581,10 +1606,19 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
             gsum += f32x4{a * d.x, a * d.y, a * d.z, gz};
             dv[4 * mb + i] = gz;
           }
+#ifdef MLP2_DIAG_FIRST_SET
+        if (it == 0) *(f32x4*)(gme + 64 * nb) = gsum; else
+#endif
         *(f32x4*)(gme + 64 * nb) += gsum;
+#ifdef MLP2_DIAG_WAIT_GME
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         dsp[nb] = split_w8(dv);
       }
       VSTAMP(6);
+#ifdef MLP2_DIAG_BAR_GME
+      __syncthreads();
+#endif
       // stage X(t+2) only now: no LDS-DMA is in flight while head / backward rows run their LDS
       // read-modify-writes (measured: with the DMA in flight across them, 1 - 18 % of launches
       // lost a dW2 partial)
@@ -1612,6 +1646,9 @@ __global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(
            vph[1], vph[2], vph[3], vph[4], vph[5], vph[6], vph[7]);
 #endif
   // ---- flush this workgroup's partial gradients + loss sums ----
+#ifdef MLP2_DIAG_BAR_FLUSH
+  __syncthreads();
+#endif
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;

@@ -367,7 +367,11 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
             ch = _try_chain(b, x_t, y_t, n_train, l2c)
             if ch is not None:
                 return ch
-        if mode == 'train' and P == 1 and os.environ.get('HPE_WIDE', '1') != '0':
+        # the wide two-layer kernels (one workgroup per launch / epoch) are opt-in: measured on
+        # MI355X they lose to the mlp2 / fit kernels for train_88.py's 88-64-3 (fused epoch b128
+        # 32.6 vs 18.3 us per step, per-step b512 68.8 vs 38.4), which spread the hidden units
+        # over many workgroups; create_model_complex (16-wide blocks) keeps the residual kernels
+        if mode == 'train' and P == 1 and os.environ.get('HPE_WIDE', '0') == '1':
             wide = _try_wide(b, x_t, y_t, n_train, l2c)
             if wide is not None:
                 return wide

@@ -60,7 +60,8 @@ def regions(d):
         if len(shp) >= 2:
             F = shp[-1]
             rows, cols = np.unique(sel // F), np.unique(sel % F)
-            out.append('%s[%d of %d: rows %s cols %s]' % (name, len(sel), sz, rows[:8].tolist(), cols[:12].tolist()))
+            pairs = ' (row, col) %s' % [(int(v // F), int(v % F)) for v in sel] if len(sel) <= 48 else ''
+            out.append('%s[%d of %d: rows %s cols %s%s]' % (name, len(sel), sz, rows[:8].tolist(), cols[:12].tolist(), pairs))
         else:
             out.append('%s[%d of %d: %s]' % (name, len(sel), sz, sel[:8].tolist()))
     tail = d[d >= eng.n_train]

@@ -62,13 +62,14 @@ def _m88(F):
 
 
 @pytest.mark.parametrize('F', [16, 32, 48, 64])
-def test_fused_kernel_programs_pass_host_validation(F):
-    """train_88.py's create_model at P = 1 compiles to the wide residual-stack kernel (KIND_RES, no
-    blocks) and hpe_program_create's host-side validation accepts it — with no GPU the call gets as
+def test_fused_kernel_programs_pass_host_validation(F, monkeypatch):
+    """train_88.py's create_model at P = 1 compiles (HPE_WIDE=1) to the wide residual-stack kernel
+    (KIND_RES, no blocks) and hpe_program_create's host-side validation accepts it — with no GPU the call gets as
     far as the device allocation (rc 2), never a geometry rejection (rc 1).  Regression: F = 64
     (5,891 parameters) once exceeded the kernels' LDS parameter capacity."""
     import numpy as np
     from hpe import compiler
+    monkeypatch.setenv('HPE_WIDE', '1')
     m = _m88(F)
     prog = compiler.compile_graph(m.model_config, m.weights_dict(), mode='train', P=1)
     assert prog.kind == 'res' and prog.info['blocks'] == 0

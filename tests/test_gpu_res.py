@@ -62,10 +62,11 @@ def _model88(F=64, dr=1e-4, opt=None, seed=88):
 
 
 @pytest.mark.parametrize('F,n,dr,gather', [(64, 512, 1e-4, False), (64, 203, 0.3, True), (32, 128, 0.2, False)])
-def test_wide_gradient_vs_float64_oracle(F, n, dr, gather):
+def test_wide_gradient_vs_float64_oracle(F, n, dr, gather, monkeypatch):
     """create_model with a narrow hidden layer at P = 1 (the wide two-layer kernel of
-    csrc/hpe_res.hip): one training launch against the float64 oracle's autograd gradient, dropout
-    on both layers; P > 1 launches keep the mlp2 kernel."""
+    csrc/hpe_res.hip, opt-in: HPE_WIDE=1): one training launch against the float64 oracle's
+    autograd gradient, dropout on both layers; P > 1 launches keep the mlp2 kernel."""
+    monkeypatch.setenv('HPE_WIDE', '1')
     m = _model88(F, dr)
     eng = m._eng()
     prog = eng.program('train', 1).prog
@@ -139,11 +140,12 @@ def test_res_gradient_repeatable():
 
 @pytest.mark.parametrize('net,opt,bs', [('complex', 'sgd', 128), ('complex', 'adam', 128), ('complex', 'adamax', 96),
                                         ('complex', 'adam', 300), ('m88', 'adam', 512), ('m88', 'sgd', 128)])
-def test_res_fused_epoch_matches_per_step_bit_for_bit(net, opt, bs):
+def test_res_fused_epoch_matches_per_step_bit_for_bit(net, opt, bs, monkeypatch):
     """fit's whole-epoch launch (res_fit_kernel: gradient, then the Keras legacy optimizer in LDS)
     against the per-step path (res_train_kernel on one workgroup + hpe_reduce_optim_step): the same
     gradient code, the same summation order and the same optimizer arithmetic, so after 3 epochs
     of BIWI_Train_Enlarged rows every weight is bit-identical."""
+    monkeypatch.setenv('HPE_WIDE', '1')   # the m88 cases: the (opt-in) wide kernels
     d = np.load(DATA + '/BIWI_Train_Enlarged_features_88_0.7_1.npz')
     x = d['features'].reshape(-1, 1, 1, 88).astype(np.float32)[:700]
     y = d['poses'].reshape(-1, 1, 1, 3)[:700]
