@@ -1734,17 +1734,25 @@ static mlp2_fn pick_w(int act, int act2) {
   return mlp2w_kernel<KH, -1, DROP>;
 }
 
-// the 8-wave 16x16x32 kernel (mlp2v_kernel) for the split launches it covers; HPE_MLP2_V=0 keeps
-// the 12-wave mlp2_kernel (A/B)
+// the 8-wave 16x16x32 kernel (mlp2v_kernel): OPT-IN (HPE_MLP2_V=1) since round 4 — its gradient is
+// not reproducible launch to launch (DESIGN.md, mlp2v open issue: rare dropped dW2 terms, a 1e-5
+// deviation of the configs[3] gradient in some processes, wrong dW2 with dropout on 8x8 maps); the
+// default is the 12-wave mlp2_kernel, which no screen has caught
 static bool mlp2_v_enabled() {
   const char* e = getenv("HPE_MLP2_V");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
-static bool use_v(const int* w, const Args& a) {
+// mlp2v only where every workgroup walks at least two tiles: at one tile per workgroup (launches of
+// fewer than 2 x grid tiles) its dW2 accumulation is not reproducible (DESIGN.md, mlp2v open
+// issue: one row's term of one 16-lane group dropped in rare launches, and with SpatialDropout on
+// the tanh instantiation wrong dW2 in most launches); those launches run the 12-wave mlp2_kernel
+static bool use_v(const int* w, const Args& a, int grid) {
   const int* o = w + w[H_OPS_OFF];
   const int ncb = o[O_MODE];
+  const int64_t ntiles = (a.nrows + 31) / 32;
   return mlp2_v_enabled() && !mlp2_one_barrier() && w[H_MODE] == MODE_TRAIN && a.P >= 32 &&
-         ncb > 4 && ncb <= MLP2_MAXW && o[O_K] <= 96;
+         ncb > 4 && ncb <= MLP2_MAXW && o[O_K] <= 96 && ntiles >= 2 * (int64_t)grid &&
+         o[O_EDROP] < 0 && o[O_TBASE] < 0;  // no SpatialDropout on either layer
 }
 template <bool DROP>
 static mlp2_fn pick_v(int act, int act2) {
@@ -1829,7 +1837,7 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
     return rc;
   }
   hpe_tev_begin(s);
-  if (use_v(w, a)) {
+  if (use_v(w, a, grid)) {
     const int* o = w + w[H_OPS_OFF];
     const mlp2_fn kv = o[O_EDROP] >= 0 ? pick_v<true>(act, o[O_AUX2]) : pick_v<false>(act, o[O_AUX2]);
     if (launch_k(kv, V_NW, v_lds_floats() * 4, a, grid, s)) return 2;

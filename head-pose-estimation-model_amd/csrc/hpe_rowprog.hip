@@ -1431,3 +1431,41 @@ extern "C" int hpe_reduce_optim_step(const hpe_program* p, int64_t n_rows, const
   HIPCHK(hipGetLastError());
   return HPE_OK;
 }
+
+// ---- hpe_fit_steps: fit's per-step path for one epoch, the step loop in C -----------------------
+// The launches fit's Python loop issues per step, in the same order with the same arguments (so the
+// results are bit-identical), without a Python round trip per step: hpe_train_step_bounded, then
+// hpe_reduce_optim_step when the launch grid is small (single rank) or hpe_reduce + hpe_optim_step.
+#define HPE_FUSED_REDUCE_MAX_GRID 16   // hpe/engine.py Engine.FUSED_REDUCE_MAX_GRID
+extern "C" int hpe_fit_steps(const hpe_program* p, float* params, float* params_t, float* m, float* v,
+                             const float* l2, const int32_t* tpos, int64_t n_train, const float* x,
+                             const float* ytrue, const int32_t* perm, int64_t n, int32_t batch, int32_t P,
+                             float x_bound, int32_t kind, float lr, float b1, float b2, float eps,
+                             uint64_t seed_base, int64_t iter0, void* ws, float* grad, float* stats,
+                             int32_t stats_stride, void* stream) {
+  if (!p || !params || !x || !ytrue || !perm || !ws || !grad || !l2 || !tpos || !stats)
+    return fail(HPE_EINVAL, "hpe_fit_steps: null argument");
+  if (n <= 0 || batch <= 0 || P <= 0 || iter0 < 0 || stats_stride < 2)
+    return fail(HPE_EINVAL, "hpe_fit_steps: bad shape n=%lld batch=%d P=%d", (long long)n, batch, P);
+  if (n_train != p->hdr[H_NPARAMS_TRAIN]) return fail(HPE_EINVAL, "hpe_fit_steps: n_train mismatch");
+  const int64_t steps = (n + batch - 1) / batch;
+  for (int64_t s = 0; s < steps; ++s) {
+    const int64_t b0 = s * batch, nb = (n - b0) < batch ? (n - b0) : batch;
+    const int64_t rows = nb * P, it = iter0 + 1 + s;
+    // inv_count as fit computes it: 1 / (nb P 3) in double, rounded to float
+    const float inv = (float)(1.0 / (double)(rows * 3));
+    int rc = hpe_train_step_bounded(p, params, params_t, x, ytrue, nb, P, perm + b0, 0, inv, seed_base + (uint64_t)it,
+                                    x_bound, ws, stream);
+    if (rc) return rc;
+    float* st = stats + s * stats_stride;
+    if (hpe_launch_grid(p, rows) <= HPE_FUSED_REDUCE_MAX_GRID) {
+      rc = hpe_reduce_optim_step(p, rows, ws, grad, kind, lr, b1, b2, eps, it, 1.f, params, params_t, m, v, l2, tpos,
+                                 n_train, st, stream);
+    } else {
+      rc = hpe_reduce(p, rows, ws, grad, stream);
+      if (!rc) rc = hpe_optim_step(kind, lr, b1, b2, eps, it, 1.f, params, params_t, m, v, grad, l2, tpos, n_train, st, stream);
+    }
+    if (rc) return rc;
+  }
+  return HPE_OK;
+}

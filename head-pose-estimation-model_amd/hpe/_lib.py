@@ -27,6 +27,8 @@ SIGNATURES = {
     'hpe_optim_grid': (ctypes.c_int, [_i64]),
     'hpe_reduce_optim_step': (ctypes.c_int, [_vp, _i64, _vp, _vp, _i32, _f, _f, _f, _f, _i64, _f, _vp, _vp, _vp,
                                              _vp, _vp, _vp, _i64, _vp, _vp]),
+    'hpe_fit_steps': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32,
+                                     _f, _i32, _f, _f, _f, _f, _u64, _i64, _vp, _vp, _vp, _i32, _vp]),
     'hpe_fit_supported': (ctypes.c_int, [_vp, _i32]),
     'hpe_fit_workspace_size': (_sz, [_vp, _i32]),
     'hpe_fit_epoch': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f,

@@ -218,6 +218,31 @@ class Engine:
     def optim_grid(self):
         return _lib.load().hpe_optim_grid(self.n_train)
 
+    def fit_steps(self, opt, x, y, perm, batch, stats, seed_base, x_bound=0.0, P=1):
+        """One epoch of fit's per-step path (single rank) as ONE C call: hpe_fit_steps issues, per
+        step, the launches gradient(defer_reduce=True) + optimizer_step issue from Python, with the
+        same arguments (bit-identical results) and no Python round trip between steps."""
+        if P > 1 and self.spatial() is not None:
+            raise ValueError('fit of attention heads runs on 1x1 maps (train_88.py:270-305)')
+        kind = OPT_KIND[opt.kind]
+        if kind and self.m is None:
+            self.m = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+            self.v = torch.zeros(self.n_train, dtype=torch.float32, device=self.device)
+        c = self.program('train', P)
+        lib = _lib.load()
+        n = int(perm.numel())
+        steps = (n + batch - 1) // batch
+        ws = c.workspace(min(batch, n) * P, self.device)
+        _lib.check(lib.hpe_fit_steps(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
+                                     _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),
+                                     n, int(batch), int(P), float(x_bound), kind, float(opt.learning_rate),
+                                     float(opt.beta_1), float(opt.beta_2), float(opt.epsilon),
+                                     int(seed_base) & 0xFFFFFFFFFFFFFFFF, int(self.iterations), _ptr(ws),
+                                     _ptr(self.grad), _ptr(stats), int(stats.shape[1]), _stream()),
+                   'hpe_fit_steps')
+        self._pending = None
+        self.iterations += steps
+
     # -- whole-epoch launch (P = 1, one rank): csrc/hpe_fit.hip ----------------------------------
     # batches above this run the per-step path unless HPE_FIT_FUSED=1: the epoch kernel computes
     # on one XCD's workgroups (hidden units split over <= 32 CUs), which wins while a step is

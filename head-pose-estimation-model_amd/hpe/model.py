@@ -280,7 +280,13 @@ class Model:
                     # the epoch launch timed out and was rolled back: this and later epochs per step
                     fused = self._last_fit_fused = False
                     stats = torch.zeros((steps, 2 + og), dtype=torch.float32, device=eng.device)
-            for s in range(0 if fused else steps):
+            # single rank, per-step path: the whole step loop in one C call (hpe_fit_steps: the same
+            # launches as the loop below, without a Python round trip per step); HPE_FIT_STEPS=0 keeps
+            # the Python loop
+            c_steps = not fused and world == 1 and os.environ.get('HPE_FIT_STEPS', '1') != '0'
+            if c_steps:
+                eng.fit_steps(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0), x_bound, P)
+            for s in range(0 if fused or c_steps else steps):
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0
                 r0, r1 = batch_slice(b0, b1, rank, world)   # this rank's share of the batch

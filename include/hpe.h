@@ -112,6 +112,20 @@ int hpe_reduce_optim_step(const hpe_program *prog, int64_t n_rows, const void *w
                           float grad_scale, float *params, float *params_t, float *m, float *v,
                           const float *l2, const int32_t *tpos, int64_t n, float *stats, void *stream);
 
+/* One epoch of model.fit's per-step path for a single rank, the step loop in C (replaces the
+ * Python step loop of Keras fit, train_96.py:175-183, for programs the whole-epoch kernel does not
+ * take: P > 1 maps, batches above its limit, every graph the fused kernels do not cover).  For
+ * s = 0 .. ceil(n / batch) - 1 with rows perm[s*batch .. min(n, (s+1)*batch)): hpe_train_step_bounded
+ * (dropout seed seed_base + iter0 + 1 + s, inv_count = (float)(1.0 / (rows * P * 3)), x_bound), then
+ * hpe_reduce_optim_step when hpe_launch_grid <= 16, else hpe_reduce + hpe_optim_step, with iteration
+ * iter0 + 1 + s and stats + s * stats_stride — the launches fit issues from Python, bit-identical. */
+int hpe_fit_steps(const hpe_program *prog, float *params, float *params_t, float *m, float *v,
+                  const float *l2, const int32_t *tpos, int64_t n_train, const float *x,
+                  const float *y_true, const int32_t *perm, int64_t n, int32_t batch, int32_t P,
+                  float x_bound, int32_t kind, float lr, float beta_1, float beta_2, float epsilon,
+                  uint64_t seed_base, int64_t iter0, void *workspace, float *grad, float *stats,
+                  int32_t stats_stride, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
  * Keras fit (train_96.py:175-183, train_88.py:355-363) for the reference's own regime: 1x1 maps
