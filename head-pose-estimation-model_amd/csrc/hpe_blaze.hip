@@ -736,34 +736,40 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
                                          const float* dwt, const float* P_, int chunk, int grp,
                                          f32x16 (&acc)[BFS_MAXNC]) {
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  const int lgWo = __builtin_ctz(o.wo);
+  // the op's fields as wave-uniform registers for the whole task (read from the kernel arguments
+  // once: left as references the compiler re-loads them from kernarg inside the K loop, and every
+  // s_load there serialises the LDS reads behind an lgkmcnt(0))
+  const int cinp = __builtin_amdgcn_readfirstlane(o.cinp), ks = __builtin_amdgcn_readfirstlane(o.ks);
+  const int coutp = __builtin_amdgcn_readfirstlane(o.coutp), nc = __builtin_amdgcn_readfirstlane(o.nc);
+  const int ow = __builtin_amdgcn_readfirstlane(o.w), wo = __builtin_amdgcn_readfirstlane(o.wo);
+  const int lgWo = __builtin_ctz(wo);
   const int p = chunk * 32 + l32;
-  const int oy = p >> lgWo, ox = p & (o.wo - 1);
+  const int oy = p >> lgWo, ox = p & (wo - 1);
   int toff[9];
   uint32_t tmask = 0;
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp) {
     const int iy = oy * o.s - o.padt + tp / 3, ix = ox * o.s - o.padl + tp % 3;
-    const bool ok = iy >= 0 && iy < o.h && ix >= 0 && ix < o.w;
-    toff[tp] = ok ? (iy * o.w + ix) * ss : 0;
+    const bool ok = iy >= 0 && iy < o.h && ix >= 0 && ix < ow;
+    toff[tp] = ok ? (iy * ow + ix) * ss : 0;
     tmask |= ok ? (1u << tp) : 0u;
   }
-  const int cen = (oy * o.w + ox) * ss;
+  const int cen = (oy * ow + ox) * ss;
 #pragma unroll
   for (int j = 0; j < BFS_MAXNC; ++j) acc[j] = (f32x16){};
-  const int n0 = grp * o.nc * 32 + l32;
+  const int n0 = grp * nc * 32 + l32;
 #pragma unroll 2
-  for (int c0 = 4 * half; c0 < o.cinp; c0 += 8) {
+  for (int c0 = 4 * half; c0 < cinp; c0 += 8) {
     f32x4 av;
     if (DW) {
       f32x4 xv[9];
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(src + toff[tp] + c0);
-      av = ld4(dwt + 9 * o.cinp + c0);
+      av = ld4(dwt + 9 * cinp + c0);
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) {
         const f32x4 x = (tmask >> tp) & 1u ? xv[tp] : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 wv = ld4(dwt + tp * o.cinp + c0);
+        const f32x4 wv = ld4(dwt + tp * cinp + c0);
         av.x = fmaf(x.x, wv.x, av.x);
         av.y = fmaf(x.y, wv.y, av.y);
         av.z = fmaf(x.z, wv.z, av.z);
@@ -774,9 +780,9 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
     }
 #pragma unroll
     for (int j = 0; j < BFS_MAXNC; ++j) {
-      if (j < o.nc) {
+      if (j < nc) {
         const int n = n0 + 32 * j;
-        const f32x4 wv = n < o.coutp ? ld4(wt + n * o.ks + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 wv = n < coutp ? ld4(wt + n * ks + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
         acc[j] = mfma_split(av, wv, acc[j]);
       }
     }
@@ -784,20 +790,20 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
   // epilogue values: lane = output channel n, registers = 16 positions of the chunk
 #pragma unroll
   for (int j = 0; j < BFS_MAXNC; ++j) {
-    if (j >= o.nc) continue;
+    if (j >= nc) continue;
     const int n = n0 + 32 * j;
-    const float bias = n < o.coutp ? P_[o.pwb + n] : 0.f;
+    const float bias = n < coutp ? P_[o.pwb + n] : 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-      const int qy = q >> lgWo, qx = q & (o.wo - 1);
+      const int qy = q >> lgWo, qx = q & (wo - 1);
       float v = acc[j][g] + bias;
       if (RES == BF_RES_ID) {
-        if (n < o.cinp) v += src[(qy * o.w + qx) * ss + n];
+        if (n < cinp) v += src[(qy * ow + qx) * ss + n];
       } else if (RES == BF_RES_MAXPOOL) {
-        if (n < o.cinp) {
-          const float* t = src + ((2 * qy) * o.w + 2 * qx) * ss + n;
-          v += fmaxf(fmaxf(t[0], t[ss]), fmaxf(t[o.w * ss], t[o.w * ss + ss]));
+        if (n < cinp) {
+          const float* t = src + ((2 * qy) * ow + 2 * qx) * ss + n;
+          v += fmaxf(fmaxf(t[0], t[ss]), fmaxf(t[ow * ss], t[ow * ss + ss]));
         }
       }
       if (DW && o.relu) v = v > 0.f ? v : 0.f;
@@ -845,12 +851,15 @@ __global__ void __launch_bounds__(BFS_NW * 64) bf_stage_kernel(BfStageArgs a) {
       const int64_t hwo = o.ho * o.wo;
       float* gd = o.gdst >= 0 ? a.bufs[o.gdst] : nullptr;
       float* gd2 = o.split ? a.bufs[o.gdst2] : nullptr;
+      const int nc = __builtin_amdgcn_readfirstlane(o.nc), coutp = __builtin_amdgcn_readfirstlane(o.coutp);
+      const int split = __builtin_amdgcn_readfirstlane(o.split), cout = __builtin_amdgcn_readfirstlane(o.cout);
+      const int ostride = __builtin_amdgcn_readfirstlane(o.ostride), lds_out = __builtin_amdgcn_readfirstlane(o.lds_out);
 #pragma unroll
       for (int j = 0; j < BFS_MAXNC; ++j) {
-        if (j >= o.nc) continue;
-        const int n = (grp * o.nc + j) * 32 + l32;
-        if (n >= o.coutp) continue;
-        if (o.lds_out) {
+        if (j >= nc) continue;
+        const int n = (grp * nc + j) * 32 + l32;
+        if (n >= coutp) continue;
+        if (lds_out) {
 #pragma unroll
           for (int g = 0; g < 16; ++g) map[(chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * cs + n] = acc[j][g];
         }
@@ -861,11 +870,11 @@ __global__ void __launch_bounds__(BFS_NW * 64) bf_stage_kernel(BfStageArgs a) {
           const float v = acc[j][g];
           {
             const int64_t pos = img * hwo + q;
-            if (o.split) {
-              if (n < o.split) gd[pos * o.split + n] = v;
-              else if (n < o.cout) gd2[pos * (o.cout - o.split) + (n - o.split)] = v;
-            } else if (n < o.ostride) {
-              gd[pos * o.ostride + n] = v;
+            if (split) {
+              if (n < split) gd[pos * split + n] = v;
+              else if (n < cout) gd2[pos * (cout - split) + (n - split)] = v;
+            } else if (n < ostride) {
+              gd[pos * ostride + n] = v;
             }
           }
         }

@@ -456,11 +456,17 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       for (int w = 0; w < MLP2_MAXW; ++w) pv[w] = w < NCB ? part[(w * T + r) * 4 + j] : 0.f;
 #pragma unroll
       for (int w = 0; w < MLP2_MAXW; ++w) z += pv[w];
-      const int64_t img = ti.of(r) + args.img_off;
-      // ACT1 >= 0 kernels are only picked for a linear head (the create_model family)
-      const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr
-                                                      ? z / e2.keep : 0.f) : z)
-                                : e_fwd(e2, args.seed, img, j, z);
+      // ACT1 >= 0 kernels are only picked for a linear head (the create_model family); the row's
+      // image and the output dropout's keep bit only when that dropout is on (uniform branch: the
+      // no-dropout head computes neither)
+      const bool d2 = ACT1 < 0 || __builtin_expect(e2.drop >= 0, 0);
+      int64_t img = 0;
+      bool k2 = true;
+      if (d2) {
+        img = ti.of(r) + args.img_off;
+        if (ACT1 >= 0) k2 = drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr;
+      }
+      const float p = ACT1 >= 0 ? (d2 ? (k2 ? z / e2.keep : 0.f) : z) : e_fwd(e2, args.seed, img, j, z);
       if (mode == MODE_FWD) {
         if (R < nrows) args.y[R * 3 + j] = p;
       } else {
@@ -472,9 +478,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
           g = SPLIT ? 2.f * err : 2.f * err * args.inv_count;
         }
         if (train) {
-          g = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr
-                                               ? g / e2.keep : 0.f) : g)
-                        : e_bwd(e2, args.seed, img, j, g, p);
+          g = ACT1 >= 0 ? (d2 ? (k2 ? g / e2.keep : 0.f) : g) : e_bwd(e2, args.seed, img, j, g, p);
           dz2[r * 4 + j] = g;
           hacc[threadIdx.x * 4 + 2] += g;
         }
