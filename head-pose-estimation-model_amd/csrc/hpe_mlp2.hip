@@ -47,6 +47,7 @@ namespace MLP2_NS {
 // fragments of the data side of split_d8 (hpe_common.h): ch = fp16(C x), cl = fp16(C x - ch), h = fp16(x)
 #define MLP2_FS 104             // row stride (halves) of the forward layout [32 rows][2 x 48]: conflict-free b128
 #define MLP2_TS 40              // row stride (halves) of the transposed layout [96 channels][32 rows]
+#define MLP2_A1W (15 * 68 + 64)  // floats of a wave's A1 park (a1_row)
 #define MLP2_PRE_HALVES (3 * 32 * MLP2_FS + 2 * 3 * 96 * MLP2_TS)  // fwd ch, cl, h + 2 parities x transposed ch, cl, h
 
 struct E2 {
@@ -157,6 +158,14 @@ __device__ __forceinline__ void split_d4(f32x4 v, h4& ch, h4& cl, h4& h) {
   cl = __builtin_convertvector(s - __builtin_convertvector(ch, f32x4), h4);
   h = __builtin_convertvector(v, h4);
 }
+// A1 park of a wave: accumulator register g's 64 lanes at row a1_row(g), 68 floats per row slot, so
+// slot t starts on bank quad t; register g takes slot g ^ ((g >> 1) & 4) (rows 8..11 on quads 12..15,
+// 12..15 on 8..11), and the head's row-on-lane b128 reads (lane r reads row (r & 3) + 4 (r >> 3),
+// quads 8 ((r >> 2) & 1) + 4 h + q of it) hit 16 distinct bank quads in every ds_read_b128 lane group
+// (stride 64: two quads, 8-way — 112 of the 142 conflict cycles per wave and tile).  15 quads of
+// padding is the least that gives 16 distinct start quads; the rows' b32 stores / reads stay
+// contiguous, and a1_row(g) of an unrolled g is an immediate offset
+__device__ __forceinline__ constexpr int a1_row(int g) { return 68 * (g ^ ((g >> 1) & 4)); }
 template <int KH>
 __device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xf, _Float16* xt, int tid, int NT) {
   for (int i = tid; i < 32 * 24; i += NT) {
@@ -223,8 +232,8 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   float* lbuf = xbuf + NXB * MLP2_XF;
   float* part = lbuf + 2 * MLP2_LAB;
   float* dz2 = part + NCB * T * 4;
-  float* a1s = dz2 + T * 4;       // [NCB][16][64]: layer-1 activations, forward -> backward
-  float* w2t = a1s + NCB * 1024;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
+  float* a1s = dz2 + T * 4;       // [NCB][MLP2_A1W]: layer-1 activations, forward -> backward (a1_row)
+  float* w2t = a1s + NCB * MLP2_A1W;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
   float* red = hacc + NCB * 256;  // [2 * MLP2_MAXW]: block reduction of the loss sums
@@ -238,6 +247,33 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   const float* W1 = args.params + o[O_W];
   const float* W2 = args.params + o[O_AUX0];
 
+  const int64_t nrows = args.nrows;
+  const int64_t ntiles = (nrows + T - 1) / T;
+  const int P = args.P;
+  const bool labels = mode != MODE_FWD;
+  // tile -> (first image, row within it), advanced incrementally (no 64-bit division per tile)
+  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = (int)(blockIdx.x * T / P);
+  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
+  // prologue: the first tile's LDS-DMA, then every parameter load in one batch ahead of any use —
+  // one memory round trip instead of eight serial ones (W1 in two halves, W2[n], b1, the W2 table
+  // twice, b2, the tile: ~16 k cycles, the largest phase of a one-tile launch, P = 1 per-step fit).
+  // The DMA goes first: hipcc's vmcnt waits count only its own (younger) loads, so they stay exact.
+  if (blockIdx.x < ntiles) stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, ti, wave, NCB, lane, Cin, labels);
+  const int nc = min(n, F - 1);
+  const float w2a = W2[nc * 3], w2b = W2[nc * 3 + 1], w2c = W2[nc * 3 + 2];
+  const int o_bias = __builtin_amdgcn_readfirstlane(o[O_BIAS]), o_aux1 = __builtin_amdgcn_readfirstlane(o[O_AUX1]);
+  const float b1r = args.params[max(o_bias, 0) + nc];
+  float w2r[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {  // the W2 table: NCB * 128 entries over NT = 64 NCB threads
+    const int i = threadIdx.x + t * NT, nn = i >> 2, j = i & 3;
+    w2r[t] = W2[min(nn, F - 1) * 3 + min(j, 2)];
+  }
+  const float b2r = args.params[max(o_aux1, 0) + min((int)threadIdx.x & 3, 2)];
+
   // ---- register-resident weights of this wave's 32 hidden columns ----
   float wreg[SPLIT ? 1 : KH];
   SplitW wsp[SPLIT ? 6 : 1];
@@ -248,14 +284,24 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   float inv1 = 1.f, s2 = 1.f;
   if constexpr (SPLIT) {
     f32x8 v[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = half * KH + 8 * s + j;
+        v[s][j] = 8 * s + j < KH ? W1[(size_t)min(k, Cin - 1) * F + nc] : 0.f;
+      }
+    }
+    // every prologue load issued above this point (the scheduler otherwise sinks W2[n], b1 and the
+    // W2 table loads to their uses, each behind its own vmcnt wait)
+    __builtin_amdgcn_sched_barrier(0);
     float mx = 0.f;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = half * KH + 8 * s + j;
-        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
-        v[s][j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
+        v[s][j] = (k < Cin && nok) ? v[s][j] : 0.f;
         mx = fmaxf(mx, fabsf(v[s][j]));
       }
     }
@@ -264,13 +310,12 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     inv1 = SPLIT_INV_C / s1;
 #pragma unroll
     for (int s = 0; s < 6; ++s) wsp[s] = split_w8(v[s] * s1);
-    const float* w2n = args.params + o[O_AUX0] + min(n, F - 1) * 3;
-    s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
+    s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2a), fabsf(w2b)), fabsf(w2c)) : 0.f, 2);
   } else {
 #pragma unroll
     for (int m = 0; m < KH; ++m) {
       const int k = half * KH + m;
-      const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
+      const float wv = W1[(size_t)min(k, Cin - 1) * F + nc];
       wreg[m] = (k < Cin && nok) ? wv : 0.f;
     }
   }
@@ -278,15 +323,16 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   {
     // the per-unit scalars live in LDS across the tile loop, not in 3 loop-carried VGPRs (the
     // 12-wave variant sits at the 168-VGPR budget; in registers they pushed a W1 fragment to scratch)
-    const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
+    const float b1 = (nok && o_bias >= 0) ? b1r : 0.f;
     if (half == 0) *(f32x4*)(colt + n * 4) = f32x4{inv1, b1, s2, 0.f};
   }
   // small tables in LDS rather than loop-carried VGPRs (the 12-wave variant is at its budget)
-  for (int i = threadIdx.x; i < NCB * 128; i += NT) {
-    const int nn = i >> 2, j = i & 3;
-    w2t[i] = (nn < F && j < 3) ? W2[nn * 3 + j] : 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int i = threadIdx.x + t * NT, nn = i >> 2, j = i & 3;
+    if (i < NCB * 128) w2t[i] = (nn < F && j < 3) ? w2r[t] : 0.f;
   }
-  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
+  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o_aux1 >= 0) ? b2r : 0.f;
   for (int i = threadIdx.x; i < NT * 4; i += NT) hacc[i] = 0.f;
 
   f32x16 dw[NKB];
@@ -295,28 +341,17 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   float dw2[3] = {0.f, 0.f, 0.f};
   float db1 = 0.f;
 
-  const int64_t nrows = args.nrows;
-  const int64_t ntiles = (nrows + T - 1) / T;
-  const int P = args.P;
-  const bool labels = mode != MODE_FWD;
   // head phase: thread it handles (row, output) items it, it + NT3, ... with NT3 a multiple of 3,
   // so its output index j (and its db2 accumulator) is the same in every tile
   const int NT3 = (NT / 3) * 3;
 
   // pad columns [C_in, 96) of both X buffers: never written by the staging, read by the forward
-  // MFMA against zero weights -> must hold zeros, not stale LDS
+  // MFMA against zero weights -> must hold zeros, not stale LDS (the DMA above writes [0, C_in))
   for (int i = threadIdx.x; i < NXB * 32 * 16; i += NT) {
     const int r = i >> 4, c = Cin + (i & 15);
     if (c < 96) xbuf[r * MLP2_XS + c] = 0.f;
   }
   __syncthreads();
-  // tile -> (first image, row within it), advanced incrementally (no 64-bit division per tile)
-  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
-  TileImg ti;
-  ti.P = P;
-  ti.img0 = (int)(blockIdx.x * T / P);
-  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
-  if (blockIdx.x < ntiles) stage_tile(args, xbuf, lbuf, (int64_t)blockIdx.x * T, ti, wave, NCB, lane, Cin, labels);
   if constexpr (PRE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar_lds();
@@ -413,7 +448,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       }
       // park A1 in LDS across the head phase (16 VGPRs fewer live through the loss epilogue)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) a1s[(wave * 16 + g) * 64 + lane] = acc[g];
+      for (int g = 0; g < 16; ++g) a1s[wave * MLP2_A1W + a1_row(g) + lane] = acc[g];
       // head partials from the parked A1 (a row-on-lane read of this wave's own LDS region, no
       // cross-lane shuffles): lane (row r = l32, half h) dots A1[r][16 h .. 16 h + 16) with the
       // matching W2 rows, the two halves are combined with one xor-32 exchange
@@ -422,7 +457,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       {
         const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
-        const float* ar = a1s + (wave * 16 + gr) * 64 + hh * 32 + 16 * half;
+        const float* ar = a1s + wave * MLP2_A1W + a1_row(gr) + hh * 32 + 16 * half;
         const float* wr = w2t + (wave * 32 + 16 * half) * 4;
         float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -511,7 +546,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       auto dz_of = [&](int g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
         const f32x4 d = *(const f32x4*)(dz2 + r * 4);
-        const float a = a1s[(wave * 16 + g) * 64 + lane];
+        const float a = a1s[wave * MLP2_A1W + a1_row(g) + lane];
         const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
         float gz, av = a;
         if (DROP) {
@@ -766,7 +801,7 @@ __device__ __forceinline__ void w_split(const float* xs, _Float16* img, int wave
 }
 
 __host__ __device__ constexpr int w_lds_floats(int ncb) {
-  return MLP2_XF + W_NLAB * MLP2_LAB + 2 * ncb * 32 * 4 + ncb * 32 * 4 + ncb * 1024 + ncb * 128 + 4 +
+  return MLP2_XF + W_NLAB * MLP2_LAB + 2 * ncb * 32 * 4 + ncb * 32 * 4 + ncb * MLP2_A1W + ncb * 128 + 4 +
          ncb * 128 + MLP2_RED + 32 * 8 + W_NIMG * W_IMG / 2;
 }
 
@@ -789,7 +824,7 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
   float* part = lbuf + W_NLAB * MLP2_LAB;         // [2][NCB][32][4] head partials
   float* dzp = part + 2 * NCB * T * 4;            // [NCB][32][4] per-wave dZ2 rows
   float* a1s = dzp + NCB * T * 4;                 // [NCB][16][64] per-wave A1 park
-  float* w2t = a1s + NCB * 1024;                  // [NCB * 32][4]
+  float* w2t = a1s + NCB * MLP2_A1W;              // [NCB * 32][4]
   float* b2t = w2t + NCB * 128;                   // [4]
   float* colt = b2t + 4;                          // [NCB * 32][4] (inv1, b1, s2, -)
   float* red = colt + NCB * 128;                  // [MLP2_RED]
@@ -918,13 +953,13 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
         acc[g] = nok ? z : 0.f;
       }
 #pragma unroll
-      for (int g = 0; g < 16; ++g) a1s[(wave * 16 + g) * 64 + lane] = acc[g];
+      for (int g = 0; g < 16; ++g) a1s[wave * MLP2_A1W + a1_row(g) + lane] = acc[g];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       {
         const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
-        const float* ar = a1s + (wave * 16 + gr) * 64 + hh * 32 + 16 * half;
+        const float* ar = a1s + wave * MLP2_A1W + a1_row(gr) + hh * 32 + 16 * half;
         const float* wr = w2t + (wave * 32 + 16 * half) * 4;
         float p0 = 0.f, p1 = 0.f, p2 = 0.f;
 #pragma unroll
@@ -1028,7 +1063,7 @@ __global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_pe
       auto dz_of = [&](int g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
         const f32x4 d = *(const f32x4*)(dzp + (wave * T + r) * 4);
-        const float a = a1s[(wave * 16 + g) * 64 + lane];
+        const float a = a1s[wave * MLP2_A1W + a1_row(g) + lane];
         const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
         float gz, av = a;
         if (DROP) {
@@ -1799,7 +1834,7 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * 1024 + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * MLP2_A1W + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
   lds_bytes = (2 * MLP2_XF + rest) * 4;
   // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
   const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;
