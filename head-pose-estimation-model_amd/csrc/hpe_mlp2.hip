@@ -217,6 +217,10 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   // buffer is then single (consumed by the split before the barrier that opens its tile)
   constexpr bool PRE = SPLIT && NWM == MLP2_MAXW;
   constexpr int NXB = PRE ? 1 : 2;
+  // A1 park: the bank-quad slots of a1_row in the 12-wave kernel; the 4-wave one keeps rows 64 floats
+  // apart (the padding would cost it a workgroup per CU: 4 -> 3 by LDS, Model-88 train 0.94 -> 1.17 ms)
+  constexpr bool PAD1 = NWM == MLP2_MAXW;
+  constexpr int A1S = PAD1 ? MLP2_A1W : 1024;
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int mode = prog[H_MODE];
@@ -233,7 +237,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   float* part = lbuf + 2 * MLP2_LAB;
   float* dz2 = part + NCB * T * 4;
   float* a1s = dz2 + T * 4;       // [NCB][MLP2_A1W]: layer-1 activations, forward -> backward (a1_row)
-  float* w2t = a1s + NCB * MLP2_A1W;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
+  float* w2t = a1s + NCB * A1S;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
   float* b2t = w2t + NCB * 128;
   float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
   float* red = hacc + NCB * 256;  // [2 * MLP2_MAXW]: block reduction of the loss sums
@@ -448,7 +452,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       }
       // park A1 in LDS across the head phase (16 VGPRs fewer live through the loss epilogue)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) a1s[wave * MLP2_A1W + a1_row(g) + lane] = acc[g];
+      for (int g = 0; g < 16; ++g) a1s[wave * A1S + (PAD1 ? a1_row(g) : 64 * g) + lane] = acc[g];
       // head partials from the parked A1 (a row-on-lane read of this wave's own LDS region, no
       // cross-lane shuffles): lane (row r = l32, half h) dots A1[r][16 h .. 16 h + 16) with the
       // matching W2 rows, the two halves are combined with one xor-32 exchange
@@ -457,7 +461,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       {
         const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
-        const float* ar = a1s + wave * MLP2_A1W + a1_row(gr) + hh * 32 + 16 * half;
+        const float* ar = a1s + wave * A1S + (PAD1 ? a1_row(gr) : 64 * gr) + hh * 32 + 16 * half;
         const float* wr = w2t + (wave * 32 + 16 * half) * 4;
         float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -546,7 +550,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       auto dz_of = [&](int g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
         const f32x4 d = *(const f32x4*)(dz2 + r * 4);
-        const float a = a1s[wave * MLP2_A1W + a1_row(g) + lane];
+        const float a = a1s[wave * A1S + (PAD1 ? a1_row(g) : 64 * g) + lane];
         const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
         float gz, av = a;
         if (DROP) {
@@ -1834,7 +1838,7 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * MLP2_A1W + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * (ncb > 4 ? MLP2_A1W : 1024) + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
   lds_bytes = (2 * MLP2_XF + rest) * 4;
   // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
   const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;
