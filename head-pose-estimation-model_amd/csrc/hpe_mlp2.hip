@@ -217,10 +217,12 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   // buffer is then single (consumed by the split before the barrier that opens its tile)
   constexpr bool PRE = SPLIT && NWM == MLP2_MAXW;
   constexpr int NXB = PRE ? 1 : 2;
-  // A1 park: the bank-quad slots of a1_row in the 12-wave kernel; the 4-wave one keeps rows 64 floats
-  // apart (the padding would cost it a workgroup per CU: 4 -> 3 by LDS, Model-88 train 0.94 -> 1.17 ms)
-  constexpr bool PAD1 = NWM == MLP2_MAXW;
-  constexpr int A1S = PAD1 ? MLP2_A1W : 1024;
+  // A1 park in the bank-quad slots of a1_row; the 4-wave kernel pays for the padding with 3-float loss
+  // accumulators (HS: [NT][3], 128 floats fewer at NT = 128) so it keeps four workgroups per CU — the
+  // 12-wave one keeps [NT][4] (3-float rows there push its tile loop over the VGPR budget)
+  constexpr bool PAD1 = true;
+  constexpr int A1S = MLP2_A1W;
+  constexpr int HS = NWM == MLP2_MAXW ? 4 : 3;
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
   const int mode = prog[H_MODE];
@@ -239,8 +241,8 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   float* a1s = dz2 + T * 4;       // [NCB][MLP2_A1W]: layer-1 activations, forward -> backward (a1_row)
   float* w2t = a1s + NCB * A1S;  // [NCB * 32][4]: W2 rows (zero past F), then b2 [4]
   float* b2t = w2t + NCB * 128;
-  float* hacc = b2t + 4;          // [NT][4]: per-thread loss / db2 accumulators (sse, sae, db2)
-  float* red = hacc + NCB * 256;  // [2 * MLP2_MAXW]: block reduction of the loss sums
+  float* hacc = b2t + 4;          // [NT][HS]: per-thread loss / db2 accumulators (sse, sae, db2)
+  float* red = hacc + NCB * 64 * HS;  // [2 * MLP2_MAXW]: block reduction of the loss sums
   float* colt = red + MLP2_RED;   // [NCB * 32][4]: per hidden unit (inv1, b1, s2, -), re-read per tile
   _Float16* xfb = (_Float16*)(colt + NCB * 128);  // PRE: [3][32][MLP2_FS] ch, cl, h; [2][3][96][MLP2_TS]
   _Float16* xtb = xfb + 3 * 32 * MLP2_FS;
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     if (i < NCB * 128) w2t[i] = (nn < F && j < 3) ? w2r[t] : 0.f;
   }
   if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o_aux1 >= 0) ? b2r : 0.f;
-  for (int i = threadIdx.x; i < NT * 4; i += NT) hacc[i] = 0.f;
+  for (int i = threadIdx.x; i < NT * HS; i += NT) hacc[i] = 0.f;
 
   f32x16 dw[NKB];
 #pragma unroll
@@ -512,14 +514,14 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
         float g = 0.f;
         if (R < nrows) {
           const float err = p - lab[r * 4 + j];
-          hacc[threadIdx.x * 4 + 0] = fmaf(err, err, hacc[threadIdx.x * 4 + 0]);
-          hacc[threadIdx.x * 4 + 1] += fabsf(err);
+          hacc[threadIdx.x * HS + 0] = fmaf(err, err, hacc[threadIdx.x * HS + 0]);
+          hacc[threadIdx.x * HS + 1] += fabsf(err);
           g = SPLIT ? 2.f * err : 2.f * err * args.inv_count;
         }
         if (train) {
           g = ACT1 >= 0 ? (d2 ? (k2 ? g / e2.keep : 0.f) : g) : e_bwd(e2, args.seed, img, j, g, p);
           dz2[r * 4 + j] = g;
-          hacc[threadIdx.x * 4 + 2] += g;
+          hacc[threadIdx.x * HS + 2] += g;
         }
       }
     }
@@ -682,13 +684,13 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     // db2: per-thread accumulators of output j = tid % 3 -> fixed-order sum
     if (threadIdx.x < 3 && o[O_AUX1] >= 0) {
       float s = 0.f;
-      for (int i = threadIdx.x; i < NT3; i += 3) s += hacc[i * 4 + 2];
+      for (int i = threadIdx.x; i < NT3; i += 3) s += hacc[i * HS + 2];
       ws[o[O_AUX1] + threadIdx.x] = s * sc;
     }
     __syncthreads();
   }
   if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const float a = wave_sum(hacc[threadIdx.x * 4 + 0]), b = wave_sum(hacc[threadIdx.x * 4 + 1]);
+  const float a = wave_sum(hacc[threadIdx.x * HS + 0]), b = wave_sum(hacc[threadIdx.x * HS + 1]);
   if (lane == 0) { red[wave] = a; red[MLP2_MAXW + wave] = b; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1838,7 +1840,7 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
   rbw = o[O_FLAGS];
   ncb = o[O_MODE];
   const int T = 32;
-  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * (ncb > 4 ? MLP2_A1W : 1024) + ncb * 128 + 4 + ncb * 256 + MLP2_RED + ncb * 128;
+  const int rest = 2 * MLP2_LAB + ncb * T * 4 + T * 4 + ncb * MLP2_A1W + ncb * 128 + 4 + ncb * 64 * (ncb > 4 ? 4 : 3) + MLP2_RED + ncb * 128;
   lds_bytes = (2 * MLP2_XF + rest) * 4;
   // the 12-wave variant's split kernel (PRE): one raw tile buffer + the pre-split halves
   const int pre = (MLP2_XF + rest) * 4 + MLP2_PRE_HALVES * 2;
