@@ -251,19 +251,15 @@ def run_train(eng, opt, x, y, P, n_local, n_global, rank, world, steps, warmup, 
 
 
 def train_kernel_name(eng, P):
-    """The kernel libhpe.so runs for a training launch of this program (csrc/hpe_mlp2.hip use_v:
-    the 12-wave mlp2_kernel; mlp2v_kernel only when opted in with HPE_MLP2_V=1, for 128 < F <= 384,
-    C_in <= 96 at P >= 32 without dropout)."""
+    """The kernel libhpe.so runs for a training launch of this program (csrc/hpe_mlp2.hip
+    launch_pair: mlp2_kernel, its fp16-split instantiation unless exact fp32 is forced)."""
     prog = eng.program('train', P).prog
     if prog.kind == 'res':
-        return 'wide_train_kernel' if prog.info.get('blocks') == 0 else 'res_train_kernel'
+        return 'res_train_kernel'
     if prog.kind != 'mlp2':
         return 'rowprog_kernel'
     if os.environ.get('HPE_EXACT_FP32') == '1':
         return 'mlp2_kernel (exact fp32)'
-    F_, cin = prog.info['F'], prog.C_in
-    if P >= 32 and 128 < F_ <= 384 and cin <= 96 and os.environ.get('HPE_MLP2_V') == '1':
-        return 'mlp2v_kernel'
     return 'mlp2_kernel'
 
 

@@ -389,13 +389,14 @@ int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
   if (hpe_exact_fp32() || !a.guard) {
     Args e = a;
     e.guard = nullptr;
-    hpe_tev_begin(s);
+    const int tv = hpe_tev_begin(s);
     const int rc = launch_one(pick<ChainExact>(o, g), e, grid, s);
-    hpe_tev_end(s);
+    hpe_tev_end(s, tv);
     return rc;
   }
-  hpe_tev_begin(s);
-  if (launch_one(pick<ChainSplit>(o, g), a, grid, s)) return 2;
-  hpe_tev_end(s);
+  const int tv = hpe_tev_begin(s);
+  const int rc = launch_one(pick<ChainSplit>(o, g), a, grid, s);
+  hpe_tev_end(s, tv);
+  if (rc) return rc;
   return launch_one(pick<ChainExact>(o, g), a, grid, s);
 }

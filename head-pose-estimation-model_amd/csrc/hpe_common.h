@@ -266,8 +266,8 @@ bool hpe_exact_fp32();
 
 // hpe_kernel_timing(): HIP events around each program launch's dominant kernel (the fp16-split
 // kernel, not its early-exit exact twin), recorded on the launch stream (hpe_rowprog.hip)
-void hpe_tev_begin(hipStream_t s);
-void hpe_tev_end(hipStream_t s);
+int hpe_tev_begin(hipStream_t s);
+void hpe_tev_end(hipStream_t s, int slot);
 
 // fused 2-layer regressor kernel (hpe_mlp2.hip)
 int mlp2_supported(const int* words);

@@ -651,9 +651,6 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     return;
   }
   // ---- flush this workgroup's partial gradients + loss sums ----
-#ifdef MLP2_DIAG_BAR_FLUSH
-  __syncthreads();
-#endif
   const int slab = prog[H_SLAB];
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
@@ -702,1059 +699,6 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   }
 }
 
-// ================================================================================================
-// mlp2w_kernel: the 12-wave fp16-split kernel (create_model with 128 < F <= 384: the headline
-// create_model(360)) with ONE workgroup barrier per 32-row tile instead of three.
-//   * X staging: waves 0..7 each own rows 4w .. 4w+3 of a tile (LDS-DMA into the single raw fp32
-//     buffer) and split exactly those rows into the tile's fp16 image (ch, cl, h fragments,
-//     row-major [32][96] with a per-row chunk rotation, wslot) after their OWN vmcnt(0): staging and
-//     splitting need no workgroup barrier.  The image serves both GEMMs: the forward reads rows
-//     (ds_read_b128), the dW1 GEMM reads X^T with the gfx950 transpose read ds_read_b64_tr_b16 —
-//     no second (transposed) copy.  Three images rotate: forward(t) / backward(t) / split(t+1).
-//   * tile t: forward(t) -> A1 parked in the wave's own LDS region, head partials -> part[t & 1];
-//     split X(t+1) (own rows) -> BARRIER -> stage X(t+2) -> head(t) computed by EVERY wave for all
-//     32 rows (12 partials per row summed in fixed wave order: bit-identical in every wave), its
-//     dZ2 written to the wave's own LDS row table -> backward(t) from the wave's own tables.
-//   * loss sums / db2 are accumulated by wave 0 only, in registers (no per-thread LDS table).
-// ================================================================================================
-#define W_FS 96                      // halves per row of a fragment image (12 chunks of 16 B)
-#define W_FRAG (32 * W_FS)           // halves per fragment image [32 rows][96]
-#define W_IMG (3 * W_FRAG)           // halves per tile image (ch, cl, h)
-#define W_NIMG 3                     // images in flight
-#define W_NLAB 3                     // label buffers in flight
-
-// slot of 16-byte chunk c (0..11) in row r: conflict-free for the forward row reads (ds_read_b128,
-// lanes = rows) and for the dW1 transposed reads (ds_read_b64_tr_b16, 4 rows x 4 chunks per half)
-__device__ __forceinline__ int wrot(int r) { return ((r >> 3) & 1) + 2 * (r >> 4); }
-__device__ __forceinline__ int wslot(int c, int rot) {
-  const int p = c + rot;
-  return p >= 12 ? p - 12 : p;
-}
-
-typedef __fp16 hf4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ h4 lds_tr16(const _Float16* p) {
-  const hf4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) hf4*)(uint32_t)(uintptr_t)p);
-  return __builtin_bit_cast(h4, v);
-}
-
-// LDS-DMA staging of rows 4w .. 4w+3 of a tile by wave w < 8 (labels by wave 0)
-__device__ __forceinline__ void w_stage(const Args& args, float* xs, float* lab, int64_t row0, const TileImg& ti,
-                                        int wave, int lane, int Cin, bool labels) {
-  if (wave >= 8) return;
-  const int64_t rem = args.nrows - 1 - row0;
-  const int last = rem < 31 ? (int)rem : 31;
-  const int P = args.P;
-  const int q = Cin >> 2;
-  if (!args.idx && P >= 32) {
-    if (labels && wave == 0) {
-#pragma unroll
-      for (int pc = 0; pc < 2; ++pc) {
-        const int slot = pc * 64 + lane;
-        const int r = min(slot >> 2, last), j = min(slot & 3, 2);
-        glds4(args.ytrue + (int64_t)ti.of(r) * 3 + j, lds_addr(lab + pc * 64));
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int r = 4 * wave + k;
-      const int64_t srow = row0 + min(r, last);
-      if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
-    }
-    return;
-  }
-  const int lr = min(lane & 31, last);
-  const int limg = ti.of(lr);
-  const int lpos = (int)(row0 + lr - (int64_t)limg * P);
-  const int lsrc = args.idx ? args.idx[limg] : limg;
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (labels && wave == 0) {
-#pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-      const int slot = pc * 64 + lane;
-      const int r = min(slot >> 2, last), j = min(slot & 3, 2);
-      const int64_t src = __shfl(lsrc, r, 64);
-      glds4(args.ytrue + src * 3 + j, lds_addr(lab + pc * 64));
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int rr = min(4 * wave + k, last);
-    const int64_t srow = (int64_t)__builtin_amdgcn_readlane(lsrc, rr) * P + __builtin_amdgcn_readlane(lpos, rr);
-    if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + (4 * wave + k) * MLP2_XS));
-  }
-}
-
-// split rows 4w .. 4w+3 of the landed raw tile into an image (wave w < 8): 4 rows x 24 f32x4
-template <int KH>
-__device__ __forceinline__ void w_split(const float* xs, _Float16* img, int wave, int lane) {
-  if (wave >= 8) return;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = lane + 64 * u;
-    if (i < 96) {
-      const int q = i / 24, rem = i - q * 24, h = rem >= 12 ? 1 : 0, m0 = 4 * (rem - 12 * h);
-      const int r = 4 * wave + q;
-      const f32x4 v = m0 < KH ? *(const f32x4*)(xs + r * MLP2_XS + KH * h + m0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      h4 ch, cl, hh;
-      split_d4(v, ch, cl, hh);
-      const int col = 48 * h + m0;
-      _Float16* d = img + r * W_FS + wslot(col >> 3, wrot(r)) * 8 + (col & 7);
-      *(h4*)(d) = ch;
-      *(h4*)(d + W_FRAG) = cl;
-      *(h4*)(d + 2 * W_FRAG) = hh;
-    }
-  }
-}
-
-__host__ __device__ constexpr int w_lds_floats(int ncb) {
-  return MLP2_XF + W_NLAB * MLP2_LAB + 2 * ncb * 32 * 4 + ncb * 32 * 4 + ncb * MLP2_A1W + ncb * 128 + 4 +
-         ncb * 128 + MLP2_RED + 32 * 8 + W_NIMG * W_IMG / 2;
-}
-
-template <int KH, int ACT1, bool DROP>
-__global__ void __launch_bounds__(MLP2_MAXW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) mlp2w_kernel(Args args) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int NKB = 3;
-  constexpr int T = 32;
-  const int* prog = args.prog;
-  const int* o = prog + prog[H_OPS_OFF];
-  const int mode = prog[H_MODE];
-  const bool train = mode == MODE_TRAIN;
-  const int Cin = o[O_K], F = o[O_N], NCB = o[O_MODE];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  const int n = wave * 32 + l32;
-  const bool nok = n < F;
-  float* xraw = lds;                              // [32][MLP2_XS] raw fp32 tile (LDS-DMA target)
-  float* lbuf = xraw + MLP2_XF;                   // [3][32][4] labels
-  float* part = lbuf + W_NLAB * MLP2_LAB;         // [2][NCB][32][4] head partials
-  float* dzp = part + 2 * NCB * T * 4;            // [NCB][32][4] per-wave dZ2 rows
-  float* a1s = dzp + NCB * T * 4;                 // [NCB][16][64] per-wave A1 park
-  float* w2t = a1s + NCB * MLP2_A1W;              // [NCB * 32][4]
-  float* b2t = w2t + NCB * 128;                   // [4]
-  float* colt = b2t + 4;                          // [NCB * 32][4] (inv1, b1, s2, -)
-  float* red = colt + NCB * 128;                  // [MLP2_RED]
-  float* hac = red + MLP2_RED;                    // [32][8] wave 0's per-row loss sums (sse, sae, db2[3])
-  _Float16* xf = (_Float16*)(hac + 32 * 8);       // [3 images][3 fragments][32][96]
-
-  E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
-  E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
-  const float inv_keep1 = 1.f / e1.keep;
-  const float* W1 = args.params + o[O_W];
-  const float* W2 = args.params + o[O_AUX0];
-
-  // register-resident W1 columns as split B fragments (as mlp2_kernel)
-  SplitW wsp[6];
-  float inv1, s2;
-  {
-    f32x8 v[6];
-    float mx = 0.f;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = half * KH + 8 * s + j;
-        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
-        v[s][j] = (8 * s + j < KH && k < Cin && nok) ? wv : 0.f;
-        mx = fmaxf(mx, fabsf(v[s][j]));
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float s1 = pow2_scale(mx, 13);
-    inv1 = SPLIT_INV_C / s1;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) wsp[s] = split_w8(v[s] * s1);
-    const float* w2n = args.params + o[O_AUX0] + min(n, F - 1) * 3;
-    s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
-    const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
-    if (half == 0) *(f32x4*)(colt + n * 4) = f32x4{inv1, b1, s2, 0.f};
-  }
-  for (int i = threadIdx.x; i < NCB * 128; i += blockDim.x) {
-    const int nn = i >> 2, j = i & 3;
-    w2t[i] = (nn < F && j < 3) ? W2[nn * 3 + j] : 0.f;
-  }
-  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
-
-  f32x16 dw[NKB];
-#pragma unroll
-  for (int s = 0; s < NKB; ++s) dw[s] = f32x16{};
-  float dw2[3] = {0.f, 0.f, 0.f};
-  float db1 = 0.f;
-  // wave 0, lanes 0..31: loss sums and db2 of its rows in LDS (the head is computed by every wave)
-  if (wave == 0 && half == 0) {
-    *(f32x4*)(hac + l32 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
-    *(f32x4*)(hac + l32 * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  bool bad = false;
-
-  const int64_t nrows = args.nrows;
-  const int ntiles = (int)((nrows + T - 1) / T);
-  const int P = args.P;
-  const bool labels = mode != MODE_FWD;
-  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
-  TileImg ti;
-  ti.P = P;
-  ti.img0 = (int)(blockIdx.x * T / P);
-  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
-  // prologue: X(0) staged + split, barrier, X(1) staged
-  const int tile0 = blockIdx.x;
-  if (tile0 < ntiles) {
-    w_stage(args, xraw, lbuf, (int64_t)tile0 * T, ti, wave, lane, Cin, labels);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    w_split<KH>(xraw, xf, wave, lane);
-  }
-  __syncthreads();
-  TileImg tn = ti;
-  tn.advance(dq, dr);
-  if (tile0 + (int)gridDim.x < ntiles)
-    w_stage(args, xraw, lbuf + MLP2_LAB, (int64_t)(tile0 + gridDim.x) * T, tn, wave, lane, Cin, labels);
-
-  int it = 0;
-  for (int tile = tile0; tile < ntiles; tile += gridDim.x, ++it, ti.advance(dq, dr)) {
-    const int64_t row0 = (int64_t)tile * T;
-    const int im = it % 3;
-    const _Float16* img = xf + im * W_IMG;
-    float* pt = part + (it & 1) * NCB * T * 4;
-
-    // ---- forward(t): Z1 = X.W1 (+b1, act, dropout), A1 parked, head partials ----
-    uint32_t dmask = 0;
-    {
-      // per-lane read offsets recomputed per tile from an opaque copy of the lane id: hoisted out
-      // of the tile loop they would hold a dozen VGPRs across it (the kernel is at its budget)
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const int rot = wrot(ln & 31);
-      const _Float16* fp = img + (ln & 31) * W_FS;
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const int off = wslot(6 * half + s, rot) * 8;
-        const SplitD xd = {*(const h8*)(fp + off), *(const h8*)(fp + W_FRAG + off), *(const h8*)(fp + 2 * W_FRAG + off)};
-        acc = mfma3_dw(xd, wsp[s], acc);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      bad |= !(fabsf(sum16(acc)) <= 3.0e38f);
-      if (DROP) {
-        if (P >= 32) {
-          const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
-          const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
-            dmask |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << g) : 0u;
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
-            dmask |= drop_hash(args.seed, e1.drop, (uint64_t)(ti.of(r) + args.img_off), n) >= e1.thr ? (1u << g) : 0u;
-          }
-        }
-      }
-      const f32x4 cs = *(const f32x4*)(colt + n * 4);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        float z = act1_f<ACT1>(e1.act, fmaf(acc[g], cs.x, cs.y));
-        if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
-        acc[g] = nok ? z : 0.f;
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) a1s[wave * MLP2_A1W + a1_row(g) + lane] = acc[g];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      {
-        const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
-        const float* ar = a1s + wave * MLP2_A1W + a1_row(gr) + hh * 32 + 16 * half;
-        const float* wr = w2t + (wave * 32 + 16 * half) * 4;
-        float p0 = 0.f, p1 = 0.f, p2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-          const f32x4 av = *(const f32x4*)(ar + i);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f32x4 w = *(const f32x4*)(wr + (i + e) * 4);
-            p0 = fmaf(av[e], w.x, p0);
-            p1 = fmaf(av[e], w.y, p1);
-            p2 = fmaf(av[e], w.z, p2);
-          }
-        }
-        p0 += xor32(p0);
-        p1 += xor32(p1);
-        p2 += xor32(p2);
-        if (half == 0) *(f32x4*)(pt + (wave * T + r) * 4) = f32x4{p0, p1, p2, 0.f};
-      }
-    }
-    // ---- split X(t+1) (own rows, after own pieces landed) ----
-    if (tile + (int)gridDim.x < ntiles) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      w_split<KH>(xraw, xf + ((it + 1) % 3) * W_IMG, wave, lane);
-    }
-    bar_lds();
-    // ---- stage X(t+2) into the raw buffer (free: every wave split X(t+1) before the barrier) ----
-    if (tile + 2 * (int)gridDim.x < ntiles) {
-      TileImg t2 = ti;
-      t2.advance(dq, dr);
-      t2.advance(dq, dr);
-      w_stage(args, xraw, lbuf + ((it + 2) % 3) * MLP2_LAB, (int64_t)(tile + 2 * gridDim.x) * T, t2, wave, lane,
-              Cin, labels);
-    }
-
-    // ---- head(t): every wave, all 32 rows (lane r, halves split the 12 partials) ----
-    {
-      const int r = l32;
-      f32x4 sp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        const int w = 6 * half + u;
-        const f32x4 pv = w < NCB ? *(const f32x4*)(pt + (w * T + r) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        sp += pv;
-      }
-      f32x4 ot;
-      ot.x = xor32(sp.x);
-      ot.y = xor32(sp.y);
-      ot.z = xor32(sp.z);
-      const f32x4 zz = half ? ot + sp : sp + ot;  // (waves 0..5) + (waves 6..11) in every lane
-      const int64_t R = row0 + r;
-      const int64_t img64 = ti.of(r) + args.img_off;
-      const float* lab = lbuf + im * MLP2_LAB;
-      f32x4 gv = {0.f, 0.f, 0.f, 0.f};
-      float esq = 0.f, eab = 0.f;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const float z = zz[j] + b2t[j];
-        const float p = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
-                                                         ? z / e2.keep : 0.f) : z)
-                                  : e_fwd(e2, args.seed, img64, j, z);
-        if (mode == MODE_FWD) {
-          if (wave == 0 && half == 0 && R < nrows) args.y[R * 3 + j] = p;
-        } else {
-          float g = 0.f;
-          if (R < nrows) {
-            const float err = p - lab[r * 4 + j];
-            esq = fmaf(err, err, esq);
-            eab += fabsf(err);
-            g = 2.f * err;
-          }
-          if (train) {
-            g = ACT1 >= 0 ? (e2.drop >= 0 ? (drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr
-                                                 ? g / e2.keep : 0.f) : g)
-                          : e_bwd(e2, args.seed, img64, j, g, p);
-          }
-          gv[j] = g;
-        }
-      }
-      if (wave == 0 && half == 0 && mode != MODE_FWD) {
-        f32x4 h0 = *(f32x4*)(hac + r * 8);
-        f32x4 h1 = *(f32x4*)(hac + r * 8 + 4);
-        h0.x += esq;
-        h0.y += eab;
-        h0.z += gv.x;
-        h0.w += gv.y;
-        h1.x += gv.z;
-        *(f32x4*)(hac + r * 8) = h0;
-        *(f32x4*)(hac + r * 8 + 4) = h1;
-      }
-      if (!train) continue;
-      if (half == 0) *(f32x4*)(dzp + (wave * T + r) * 4) = gv;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-
-    // ---- backward(t): dZ1 in registers, dW1 += X^T.dZ1 with X^T by transposed reads ----
-    {
-      const f32x4 w2v = *(const f32x4*)(w2t + n * 4);
-      const float s2n = colt[n * 4 + 2];
-      auto dz_of = [&](int g) {
-        const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
-        const f32x4 d = *(const f32x4*)(dzp + (wave * T + r) * 4);
-        const float a = a1s[wave * MLP2_A1W + a1_row(g) + lane];
-        const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
-        float gz, av = a;
-        if (DROP) {
-          gz = (dmask >> g) & 1u ? da * inv_keep1 : 0.f;
-          av = a * e1.keep;
-        } else {
-          gz = da;
-        }
-        gz = nok ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
-        dw2[0] = fmaf(a, d.x, dw2[0]);
-        dw2[1] = fmaf(a, d.y, dw2[1]);
-        dw2[2] = fmaf(a, d.z, dw2[2]);
-        db1 += gz;
-        return gz;
-      };
-      // transposed reads: a group of 16 lanes covers 16 channels; lane 4q + p gives the address of
-      // row q (of 4), channels 4p .. 4p+3 (offsets from an opaque lane id, as in the forward)
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const int tq = (ln & 15) >> 2, tp = ln & 3;
-      const int tcc = 2 * ((ln >> 4) & 1) + (tp >> 1);     // chunk within a 32-channel block (0..3)
-      const int tbase = (4 * (ln >> 5) + tq) * W_FS + 4 * (tp & 1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f32x8 dv;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          dv[j] = dz_of(8 * s + j);
-          if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-        const SplitW dsp = split_w8(dv * s2n);
-        // rows 16 s + 4 h + q (elements 0..3) and 16 s + 8 + 4 h + q (4..7): rotations 2 s, 2 s + 1
-        const _Float16* ra = img + tbase + 16 * s * W_FS;
-        const _Float16* rb = ra + 8 * W_FS;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          const int oa = wslot(4 * kb + tcc, 2 * s) * 8, ob = wslot(4 * kb + tcc, 2 * s + 1) * 8;
-          SplitD xd;
-          xd.ch = __builtin_shufflevector(lds_tr16(ra + oa), lds_tr16(rb + ob), 0, 1, 2, 3, 4, 5, 6, 7);
-          xd.cl = __builtin_shufflevector(lds_tr16(ra + W_FRAG + oa), lds_tr16(rb + W_FRAG + ob), 0, 1, 2, 3, 4, 5, 6, 7);
-          xd.h = __builtin_shufflevector(lds_tr16(ra + 2 * W_FRAG + oa), lds_tr16(rb + 2 * W_FRAG + ob), 0, 1, 2, 3, 4, 5, 6, 7);
-          dw[kb] = mfma3_dw(xd, dsp, dw[kb]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-  }
-
-  if (mode == MODE_FWD) {
-    if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // ---- flush this workgroup's partial gradients + loss sums ----
-#ifdef MLP2_DIAG_BAR_FLUSH
-  __syncthreads();
-#endif
-  const int slab = prog[H_SLAB];
-  const int npt = prog[H_NPARAMS_TRAIN];
-  float* ws = args.ws + (size_t)blockIdx.x * slab;
-  const float sc = args.inv_count;
-  if (train) {
-    const float s2f = colt[n * 4 + 2];
-    float chk = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-      chk += sum16(dw[kb]);
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        // image position -> channel (KH = 44: positions 44..47 / 92..95 are padding)
-        const int kp = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        const int kh = kp >= 48 ? kp - 48 : kp;
-        const int k = (kp >= 48 ? KH : 0) + kh;
-        if (kh < KH && k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (sc * (SPLIT_INV_C / s2f));
-      }
-    }
-    bad |= !(fabsf(chk) <= 3.0e38f);
-    const float tb = db1 + __shfl_xor(db1, 32, 64);
-    float t2[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
-    if (half == 0 && nok) {
-      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
-    }
-  }
-  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (wave == 0) {
-    const f32x4 h0 = half == 0 ? *(const f32x4*)(hac + l32 * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const float h1 = half == 0 ? hac[l32 * 8 + 4] : 0.f;
-    const float a = wave_sum(h0.x), b = wave_sum(h0.y);
-    const float d0 = wave_sum(h0.z), d1 = wave_sum(h0.w), d2 = wave_sum(h1);
-    if (lane == 0) {
-      ws[npt] = a;
-      ws[npt + 1] = b;
-      if (train && o[O_AUX1] >= 0) {
-        ws[o[O_AUX1] + 0] = d0 * sc;
-        ws[o[O_AUX1] + 1] = d1 * sc;
-        ws[o[O_AUX1] + 2] = d2 * sc;
-      }
-    }
-  }
-}
-
-// ================================================================================================
-// mlp2v_kernel: create_model with 128 < F <= 384 and C_in <= 96 (the headline create_model(360)) on
-// v_mfma_f32_16x16x32_f16 (the fp16 split of hpe_common.h at fp32 accuracy), 8 waves of 48 hidden
-// units, two per SIMD: a 256-register budget holds W1 (72 VGPRs of split B fragments), the dW1
-// accumulators (72) and a whole tile's Z1 (24) without spilling.  ONE workgroup barrier per
-// 32-row tile, and no phase in which most waves wait for a few (the 12-wave kernel runs three
-// lock-step phases per tile and a 96-item head on two waves).
-//   * staging (v_stage): wave w LDS-DMAs rows 4w .. 4w+3 of tile t+2 into the raw fp32 tile
-//     (labels: wave 0) after its backward rows of tile t and, one tile later, splits exactly those
-//     rows into the fp16 images after its own vmcnt(0) (an LDS-DMA is ordered for the issuing
-//     wave's ds_read by its vmcnt alone) — staging and splitting need no workgroup barrier.  No DMA
-//     is in flight while the head / backward rows run their LDS read-modify-writes: issued before
-//     the barrier (across them), 1-18 % of launches lost a dW2 partial (race screens on MI355X);
-//   * fp16 images (fragments ch, cl, h of split_d8 each), both read conflict-free by ds_read_b128:
-//       forward    xf[row][96]: the 16-B chunk c of row r at c ^ ((r >> 1) & 3);
-//       transposed xt[ch][32]:  in the dW1 GEMM's K order, position 8g + j <-> tile row
-//                  16 (j >> 2) + 4g + (j & 3) (the rows the forward accumulator of lane group g
-//                  holds), chunk g of channel ch at g ^ f((ch >> 2) & 3), f = {0, 2, 3, 1};
-//   * tile t: forward Z1 = X.W1 (2 row blocks x 3 column blocks x 3 K-steps, 3 MFMAs each), act,
-//     head partials over the wave's 48 units (in-lane over the 3 column blocks, then a DPP
-//     reduce-scatter over the 16 lanes of a row group) -> part[t & 1]; split X(t+1); BARRIER;
-//     head(t) by EVERY wave for all 32 rows (8 partials summed in fixed wave order:
-//     the same bits in every wave), dZ2 to the wave's own LDS table; backward: dZ1 in registers
-//     straight from the forward accumulators (lane group g's rows are the K slice 8g .. 8g+7 of
-//     the dW1 GEMM) as the B operand of dW1 += X^T.dZ1, A = X^T from xt; stage X(t+2) between
-//     the backward rows and the dW1 MFMAs.
-//   Scope: training launches with P >= 32 (at most two images per tile: the configs[3] / Model-96
-//   96x96 step, contiguous or gathered by fit); evaluation, forward and P < 32 launches keep
-//   mlp2_kernel (the branches they need cost this kernel registers it does not have).
-//   Hazards (one barrier): xf has 2 buffers, xt 3 (split(t+1) runs while slower waves may still
-//   read xt(t-1) in backward(t-1)), part 2, labels 4; the raw tile rows of wave w are only ever
-//   touched by wave w.
-// ================================================================================================
-#define V_NW 8                 // waves per workgroup (48 hidden units each: F <= 384)
-#define V_XS 96                // row stride (floats) of the raw tile: a wave's 4 rows are one 1.5 KB run
-#define V_FRAGF (32 * 96)      // halves per forward-image fragment [32 rows][96 channels]
-#define V_FRAGT (96 * 32)      // halves per transposed-image fragment [96 channels][32 positions]
-
-// forward image: halves offset of 16-B chunk c of row r
-__device__ __forceinline__ int vf_off(int r, int c) { return r * 96 + 8 * (c ^ ((r >> 1) & 3)); }
-// transposed image: halves offset of chunk g (positions 8g .. 8g+7) of channel ch
-__device__ __forceinline__ int vt_off(int ch, int g) { return ch * 32 + 8 * (g ^ ((0x78 >> (2 * ((ch >> 2) & 3))) & 3)); }
-
-__host__ __device__ constexpr int v_lds_floats() {
-  return 32 * V_XS + 4 * MLP2_LAB + 2 * V_NW * 32 * 4 + V_NW * 32 * 4 + 2 * V_NW * 48 * 4 + 4 +
-         V_NW * 4 * 48 * 4 + 32 * 8 + (2 * 3 * V_FRAGF + 3 * 3 * V_FRAGT) / 2;
-}
-
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-
-// LDS-DMA staging of rows 4w .. 4w+3 of a tile by wave w (labels by wave 0); at P >= 32 a tile
-// spans at most two images, so a gathered batch (fit: args.idx) needs two uniform index loads per
-// tile, not one per row; rows past the end repeat the last row (their gradient is zero)
-__device__ __forceinline__ void v_stage(const Args& args, float* xs, float* lab, int64_t row0, const TileImg& ti,
-                                        int wave, int lane, int Cin) {
-  const int64_t rem = args.nrows - 1 - row0;
-  const int last = rem < 31 ? (int)rem : 31;
-  const int P = args.P;
-  int64_t s0 = ti.img0, s1 = ti.img0 + 1;
-  if (args.idx) {
-    const int nimg = (int)(args.nrows / P);
-    s0 = args.idx[ti.img0];
-    s1 = ti.img0 + 1 < nimg ? args.idx[ti.img0 + 1] : s0;
-  }
-  // lane id recomputed here (v_mbcnt), not carried: a loop-carried per-lane address spilled to
-  // scratch makes every piece below wait (vmcnt) for the pieces issued before it
-  int ln = __lane_id();
-  asm volatile("" : "+v"(ln));  // opaque: nothing derived from it is hoisted out of the tile loop
-  if (wave == 0) {
-#pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
-      const int slot = pc * 64 + ln;
-      const int r = min(slot >> 2, last), j = min(slot & 3, 2);
-      glds4(args.ytrue + (ti.rem0 + r >= P ? s1 : s0) * 3 + j, lds_addr(lab + pc * 64));
-    }
-  }
-  const int t0 = ti.rem0 + 4 * wave;
-  if (Cin == 96 && 4 * wave + 3 <= last && (t0 + 3 < P || t0 >= P)) {
-    // the wave's 4 rows are one 1,536-B run in HBM and in the raw tile: two pieces, not four
-    // (each LDS-DMA issue costs ~100 cycles)
-    const float* src = args.x + (t0 >= P ? s1 * P + (t0 - P) : s0 * P + t0) * 96;
-    glds16(src + 4 * ln, lds_addr(xs + 4 * wave * V_XS));
-    if (ln < 32) glds16(src + 256 + 4 * ln, lds_addr(xs + 4 * wave * V_XS + 256));
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int r = 4 * wave + k;
-    const int t = ti.rem0 + min(r, last);
-    const int64_t srow = t >= P ? s1 * P + (t - P) : s0 * P + t;
-    if (ln < (Cin >> 2)) glds16(args.x + srow * Cin + 4 * ln, lds_addr(xs + r * V_XS));
-  }
-}
-
-// split rows 4w .. 4w+3 of the landed raw tile (wave w) into both images; lane l < 48 takes
-// channels 2l, 2l+1 (pad channels of the raw tile hold zeros)
-__device__ __forceinline__ void v_split(const float* xs, _Float16* xf, _Float16* xt, int wave) {
-  int lane = __lane_id();
-  asm volatile("" : "+v"(lane));  // recomputed per call, not a loop-carried (spillable) address
-  if (lane >= 48) return;
-  const int c0 = 2 * lane;
-  h2 ch[4], cl[4], hh[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = 4 * wave + q;
-    const float2 v = *(const float2*)(xs + r * V_XS + c0);
-    const float s0 = v.x * SPLIT_C, s1 = v.y * SPLIT_C;
-    ch[q] = h2{(_Float16)s0, (_Float16)s1};
-    cl[q] = h2{(_Float16)(s0 - (float)ch[q].x), (_Float16)(s1 - (float)ch[q].y)};
-    hh[q] = h2{(_Float16)v.x, (_Float16)v.y};
-    const int off = vf_off(r, c0 >> 3) + (c0 & 7);
-    *(h2*)(xf + off) = ch[q];
-    *(h2*)(xf + V_FRAGF + off) = cl[q];
-    *(h2*)(xf + 2 * V_FRAGF + off) = hh[q];
-  }
-  // rows 4w + q -> positions 8 (w & 3) + 4 (w >> 2) + q: half a chunk per channel
-  const int g = wave & 3, p = 4 * (wave >> 2);
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int off = vt_off(c0 + e, g) + p;
-    *(h4*)(xt + off) = h4{ch[0][e], ch[1][e], ch[2][e], ch[3][e]};
-    *(h4*)(xt + V_FRAGT + off) = h4{cl[0][e], cl[1][e], cl[2][e], cl[3][e]};
-    *(h4*)(xt + 2 * V_FRAGT + off) = h4{hh[0][e], hh[1][e], hh[2][e], hh[3][e]};
-  }
-}
-
-// acc += C (D.W) on v_mfma_f32_16x16x32_f16, data fragments as A (rows), weights as B
-__device__ __forceinline__ f32x4 mfma3_16(const SplitD& d, const SplitW& w, f32x4 acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(d.cl, w.h, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(d.h, w.cl, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(d.ch, w.h, acc, 0, 0, 0);
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-
-template <int ACT1, bool DROP>
-__global__ void __launch_bounds__(V_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) mlp2v_kernel(Args args) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int T = 32;
-  const int* prog = args.prog;
-  const int* o = prog + prog[H_OPS_OFF];
-  const int Cin = o[O_K], F = o[O_N];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  const int lg = lane >> 4, lc = lane & 15;  // MFMA lane group (K slice / row quad), column in a block
-  float* xraw = lds;                         // [32][V_XS] raw fp32 tile (LDS-DMA target)
-  float* lbuf = xraw + 32 * V_XS;              // [4][32][4] labels
-  float* part = lbuf + 4 * MLP2_LAB;         // [2][V_NW][32][4] head partials
-  float* dzt = part + 2 * V_NW * T * 4;      // [V_NW][32][4] per-wave dZ2 rows
-  float* colt = dzt + V_NW * T * 4;          // [V_NW * 48][4] (inv1, b1, s2, -) per hidden unit
-  float* w2t = colt + V_NW * 48 * 4;         // [V_NW * 48][4] W2 rows (zero past F)
-  float* b2t = w2t + V_NW * 48 * 4;          // [4]
-  float* gacc = b2t + 4;                     // [V_NW][4 lane groups][48][4] (dW2 row, db1) partial sums
-  float* hac = gacc + V_NW * 4 * 48 * 4;     // [32][8] wave 0's per-row loss sums (sse, sae, db2[3])
-  _Float16* xf = (_Float16*)(hac + 32 * 8);  // [2][3][32][96]
-  _Float16* xt = xf + 2 * 3 * V_FRAGF;       // [3][3][96][32]
-
-  E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
-  E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
-  const float inv_keep1 = 1.f / e1.keep;
-  const float* W1 = args.params + o[O_W];
-  const float* W2 = args.params + o[O_AUX0];
-  const int n0 = wave * 48 + lc;  // hidden unit of column block nb: n0 + 16 nb
-
-  // ---- W1 columns as split B fragments: lane (g, c) of block nb holds column n0 + 16 nb, K
-  // elements 32 ks + 8 g + j; per-unit power-of-two scales as mlp2_kernel ----
-  SplitW wsp[3][3];  // [K-step][column block]
-#pragma unroll
-  for (int nb = 0; nb < 3; ++nb) {
-    const int n = n0 + 16 * nb;
-    const bool nok = n < F;
-    f32x8 v[3];
-    float mx = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * ks + 8 * lg + j;
-        const float wv = W1[(size_t)min(k, Cin - 1) * F + min(n, F - 1)];
-        v[ks][j] = (k < Cin && nok) ? wv : 0.f;
-        mx = fmaxf(mx, fabsf(v[ks][j]));
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, xor32(mx));
-    const float s1 = pow2_scale(mx, 13);
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) wsp[ks][nb] = split_w8(v[ks] * s1);
-    if (lg == 0) {
-      const float* w2n = W2 + min(n, F - 1) * 3;
-      const float s2 = pow2_scale(nok ? fmaxf(fmaxf(fabsf(w2n[0]), fabsf(w2n[1])), fabsf(w2n[2])) : 0.f, 2);
-      const float b1 = (nok && o[O_BIAS] >= 0) ? args.params[o[O_BIAS] + n] : 0.f;
-      // tanh: 2 log2(e) folded into the pre-activation affine (z' = 2 log2(e) z feeds exp2 directly)
-      const float kz = ACT1 == ACT_TANH ? 2.8853900817779268f : 1.f;
-      *(f32x4*)(colt + n * 4) = f32x4{(SPLIT_INV_C / s1) * kz, b1 * kz, s2, 0.f};
-      *(f32x4*)(w2t + n * 4) = nok ? f32x4{w2n[0], w2n[1], w2n[2], 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  if (threadIdx.x < 4) b2t[threadIdx.x] = (threadIdx.x < 3 && o[O_AUX1] >= 0) ? args.params[o[O_AUX1] + threadIdx.x] : 0.f;
-  // pad channels [C_in, 96) of the raw tile: never written by the staging, split into zeros
-  for (int i = threadIdx.x; i < 32 * 96; i += V_NW * 64) {
-    const int r = i / 96, c = i - r * 96;
-    if (c >= Cin) xraw[r * V_XS + c] = 0.f;
-  }
-
-  f32x4 dw[6][3];  // dW1 blocks [channel block][column block]
-#pragma unroll
-  for (int cb = 0; cb < 6; ++cb)
-#pragma unroll
-    for (int nb = 0; nb < 3; ++nb) dw[cb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // dW2 / db1 partial sums per (lane group, unit) and wave 0's loss sums live in LDS, not in 17
-  // loop-carried VGPRs (the kernel sits at its 256-register budget)
-  float* gme = gacc + ((wave * 4 + lg) * 48 + lc) * 4;  // + 64 nb: this lane's (unit, group) slot
-#ifdef MLP2_DIAG_ZERO_LOOP
-  for (int i = threadIdx.x; i < V_NW * 4 * 48 * 4; i += V_NW * 64) gacc[i] = 0.f;
-#else
-#pragma unroll
-  for (int nb = 0; nb < 3; ++nb) *(f32x4*)(gme + 64 * nb) = f32x4{0.f, 0.f, 0.f, 0.f};
-#endif
-  if (wave == 0 && half == 0) {
-    *(f32x4*)(hac + l32 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
-    *(f32x4*)(hac + l32 * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  bool bad = false;
-
-  const int64_t nrows = args.nrows;
-  const int ntiles = (int)((nrows + T - 1) / T);
-  const int P = args.P;
-  const int G = gridDim.x;
-  const int S = G * T, dq = S / P, dr = S - dq * P;
-  TileImg ti;
-  ti.P = P;
-  ti.img0 = (int)(blockIdx.x * T / P);
-  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
-  const int tile0 = blockIdx.x;
-  __syncthreads();  // pad zeros and the tables before any staging / split
-  if (tile0 < ntiles) {
-    v_stage(args, xraw, lbuf, (int64_t)tile0 * T, ti, wave, lane, Cin);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    v_split(xraw, xf, xt, wave);
-  }
-  __syncthreads();
-  {
-    TileImg tn = ti;
-    tn.advance(dq, dr);
-    if (tile0 + G < ntiles) v_stage(args, xraw, lbuf + MLP2_LAB, (int64_t)(tile0 + G) * T, tn, wave, lane, Cin);
-  }
-
-#ifdef MLP2_STAMPS
-  uint32_t vph[8] = {};
-  uint64_t vprev = __builtin_amdgcn_s_memtime();
-#define VSTAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); vph[i] += (uint32_t)(t_ - vprev); vprev = t_; } while (0)
-#else
-#define VSTAMP(i) do {} while (0)
-#endif
-  int it = 0;
-  for (int tile = tile0; tile < ntiles; tile += G, ++it, ti.advance(dq, dr)) {
-    const int64_t row0 = (int64_t)tile * T;
-    const _Float16* fimg = xf + (it & 1) * 3 * V_FRAGF;
-    const _Float16* timg = xt + (it % 3) * 3 * V_FRAGT;
-    float* pt = part + (it & 1) * V_NW * T * 4;
-
-    // ---- forward(t): Z1 = X.W1 -> act (+ dropout) in the accumulators; rows 16 mb + 4 g + i ----
-    f32x4 acc[2][3];
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 3; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        const int off = vf_off(16 * mb + lc, 4 * ks + lg);
-        const SplitD xd = {*(const h8*)(fimg + off), *(const h8*)(fimg + V_FRAGF + off), *(const h8*)(fimg + 2 * V_FRAGF + off)};
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) acc[mb][nb] = mfma3_16(xd, wsp[ks][nb], acc[mb][nb]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    VSTAMP(0);
-    {
-      float chk = 0.f;
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) chk += (acc[mb][nb][0] + acc[mb][nb][1]) + (acc[mb][nb][2] + acc[mb][nb][3]);
-      bad |= !(fabsf(chk) <= 3.0e38f);
-    }
-    uint32_t dmask = 0;  // keep bit of (mb, nb, i): 12 mb + 4 nb + i
-    if (DROP) {
-#pragma unroll
-      for (int nb = 0; nb < 3; ++nb) {
-        const int n = n0 + 16 * nb;
-        const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
-        const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 16 * mb + 4 * lg + i;
-            dmask |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << (12 * mb + 4 * nb + i)) : 0u;
-          }
-      }
-    }
-    {
-      const f32x4 cs0 = *(const f32x4*)(colt + n0 * 4), cs1 = *(const f32x4*)(colt + (n0 + 16) * 4),
-                  cs2 = *(const f32x4*)(colt + (n0 + 32) * 4);
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) {
-          const f32x4 cs = nb == 0 ? cs0 : (nb == 1 ? cs1 : cs2);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float zp = fmaf(acc[mb][nb][i], cs.x, cs.y);
-            float z = ACT1 == ACT_TANH ? fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(zp)), 1.f)
-                                       : act1_f<ACT1>(e1.act, zp);
-            if (DROP) z = (dmask >> (12 * mb + 4 * nb + i)) & 1u ? z * inv_keep1 : 0.f;
-            // act(0) = 0 for the compiled-in activations: units past F (zero W1 column, b1, W2
-            // row) come out 0 without a mask
-            acc[mb][nb][i] = (ACT1 >= 0 || n0 + 16 * nb < F) ? z : 0.f;
-          }
-        }
-    }
-    // this wave's LDS-DMA of X(t+1) (and, wave 0, its labels) lands before the wave's first LDS
-    // write of the tile: with the DMA still in flight (the prologue's X(tile0 + G) is issued just
-    // before forward(0)) a head-partial write was lost once in ~3,000 launches (race screen)
-    if (tile + G < ntiles) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // head partials of this wave's 48 units, one row block at a time: in-lane over the 3 column
-    // blocks (12 values (i, j)), then a DPP reduce-scatter over the 16 lanes c of a row group —
-    // row_half_mirror (c <-> c ^ 7) splits the row pairs, quad_perm xor 2 the rows of a pair,
-    // quad_perm xor 1 and row_ror:8 complete the sum; lane c ends with row 16 mb + 4 g +
-    // 2 ((c >> 2) & 1) + ((c >> 1) & 1), all three outputs
-    {
-      const f32x4 w0 = *(const f32x4*)(w2t + n0 * 4), w1 = *(const f32x4*)(w2t + (n0 + 16) * 4),
-                  w2 = *(const f32x4*)(w2t + (n0 + 32) * 4);
-      const bool b2 = lc & 4, b1 = lc & 2;
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
-        float v[12];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            v[3 * i + j] = fmaf(acc[mb][2][i], w2[j], fmaf(acc[mb][1][i], w1[j], acc[mb][0][i] * w0[j]));
-        float t6[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const float keep = b2 ? v[6 + k] : v[k], send = b2 ? v[k] : v[6 + k];
-          t6[k] = keep + dppf<0x141>(send);
-        }
-        float s3[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const float keep = b1 ? t6[3 + j] : t6[j], send = b1 ? t6[j] : t6[3 + j];
-          s3[j] = keep + dppf<0x4E>(send);
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          s3[j] += dppf<0xB1>(s3[j]);
-          s3[j] += dppf<0x128>(s3[j]);
-        }
-        const int rr = 16 * mb + 4 * lg + 2 * ((lc >> 2) & 1) + ((lc >> 1) & 1);
-        if ((lc & 9) == 0) *(f32x4*)(pt + (wave * T + rr) * 4) = f32x4{s3[0], s3[1], s3[2], 0.f};
-      }
-    }
-    VSTAMP(1);
-    // ---- split X(t+1) (own rows, after own pieces landed); X(t+2) is staged into the same raw
-    // rows after the backward rows below; labels rotate over 4 buffers ----
-    if (tile + G < ntiles) {
-      v_split(xraw, xf + ((it + 1) & 1) * 3 * V_FRAGF, xt + ((it + 1) % 3) * 3 * V_FRAGT, wave);
-    }
-    VSTAMP(2);
-    VSTAMP(3);
-    bar_lds();
-    VSTAMP(4);
-    // ---- head(t): every wave, all 32 rows (lane r, halves take waves 0..3 / 4..7) ----
-    {
-      const int r = l32;
-      // the four partials read before summing (one LDS round trip, not four), summed in wave order
-      f32x4 pu[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pu[u] = *(const f32x4*)(pt + ((4 * half + u) * T + r) * 4);
-      const f32x4 sp = ((pu[0] + pu[1]) + pu[2]) + pu[3];
-      f32x4 ot;
-      ot.x = xor32(sp.x);
-      ot.y = xor32(sp.y);
-      ot.z = xor32(sp.z);
-      ot.w = 0.f;
-      const f32x4 zz = half ? ot + sp : sp + ot;  // (waves 0..3) + (waves 4..7) in every lane
-      const int64_t R = row0 + r;
-      const float* lab = lbuf + (it & 3) * MLP2_LAB;
-      f32x4 gv = {0.f, 0.f, 0.f, 0.f};
-      float esq = 0.f, eab = 0.f;
-      // the output SpatialDropout's keep bits only when it is on (uniform branch: the row's image
-      // and its hash are not computed every tile for the common no-dropout head); P >= 32 here, so
-      // a row's image is img0 or img0 + 1
-      const bool d2 = ACT1 < 0 || __builtin_expect(e2.drop >= 0, 0);
-      int64_t img64 = 0;
-      uint32_t k2 = 7u;
-      if (d2) {
-        img64 = ti.img0 + (ti.rem0 + r >= P ? 1 : 0) + args.img_off;
-        if (ACT1 >= 0) {
-          k2 = 0u;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) k2 |= drop_hash(args.seed, e2.drop, (uint64_t)img64, j) >= e2.thr ? 1u << j : 0u;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const float z = zz[j] + b2t[j];
-        float p = z;
-        if (ACT1 < 0) p = e_fwd(e2, args.seed, img64, j, z);
-        else if (d2) p = (k2 >> j) & 1u ? z / e2.keep : 0.f;
-        float g = 0.f;
-        if (R < nrows) {
-          const float err = p - lab[r * 4 + j];
-          esq = fmaf(err, err, esq);
-          eab += fabsf(err);
-          g = 2.f * err;
-        }
-        if (ACT1 < 0) g = e_bwd(e2, args.seed, img64, j, g, p);
-        else if (d2) g = (k2 >> j) & 1u ? g / e2.keep : 0.f;
-        gv[j] = g;
-      }
-      if (wave == 0 && half == 0) {
-        f32x4 h0 = *(f32x4*)(hac + r * 8);
-        f32x4 h1 = *(f32x4*)(hac + r * 8 + 4);
-        h0 += f32x4{esq, eab, gv.x, gv.y};
-        h1.x += gv.z;
-        *(f32x4*)(hac + r * 8) = h0;
-        *(f32x4*)(hac + r * 8 + 4) = h1;
-      }
-      if (half == 0) *(f32x4*)(dzt + (wave * T + r) * 4) = gv;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-
-    VSTAMP(5);
-    // ---- backward(t): dZ1 (K slice of lane group g) as the B operand of dW1 += X^T.dZ1 ----
-    {
-      // one column block at a time: its 8 rows' dZ2 re-read per block through an opaque zero offset
-      // (no CSE across blocks: held for all three they would pin 32 VGPRs through the phase that
-      // sets the kernel's register peak), which the scheduler may still issue early (3.45 -> 3.34 ms
-      // against a full memory clobber between blocks)
-      SplitW dsp[3];
-#pragma unroll
-      for (int nb = 0; nb < 3; ++nb) {
-        const int n = n0 + 16 * nb;
-        // W2 row scaled by the unit's power of two s2 (the dZ1 B-fragment scale): dA1, dZ1 and the
-        // db1 sum come out scaled by s2 exactly (unscaled at the flush)
-        const f32x4 w2v = *(const f32x4*)(w2t + n * 4) * colt[n * 4 + 2];
-        f32x8 dv;
-        f32x4 gsum = {0.f, 0.f, 0.f, 0.f};  // this tile's (dW2 row, db1) of the lane's 8 rows
-        int zo = 0;
-        asm volatile("" : "+v"(zo));
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const f32x4 d = *(const f32x4*)(dzt + zo + (wave * T + 16 * mb + 4 * lg + i) * 4);
-            const float a = acc[mb][nb][i];
-            const float da = d.x * w2v.x + d.y * w2v.y + d.z * w2v.z;
-            float gz, av = a;
-            if (DROP) {
-              gz = (dmask >> (12 * mb + 4 * nb + i)) & 1u ? da * inv_keep1 : 0.f;
-              av = a * e1.keep;
-            } else {
-              gz = da;
-            }
-            // units past F: zero W2 row, so gz = 0 (act(0) = 0 for the compiled-in activations)
-            gz = (ACT1 >= 0 || n < F) ? gz * act1_g<ACT1>(e1.act, av) : 0.f;
-            gsum += f32x4{a * d.x, a * d.y, a * d.z, gz};
-            dv[4 * mb + i] = gz;
-          }
-#ifdef MLP2_DIAG_FIRST_SET
-        if (it == 0) *(f32x4*)(gme + 64 * nb) = gsum; else
-#endif
-        *(f32x4*)(gme + 64 * nb) += gsum;
-#ifdef MLP2_DIAG_WAIT_GME
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-        dsp[nb] = split_w8(dv);
-      }
-      VSTAMP(6);
-#ifdef MLP2_DIAG_BAR_GME
-      __syncthreads();
-#endif
-      // stage X(t+2) only now: no LDS-DMA is in flight while head / backward rows run their LDS
-      // read-modify-writes (measured: with the DMA in flight across them, 1 - 18 % of launches
-      // lost a dW2 partial)
-      if (tile + 2 * G < ntiles) {
-        TileImg t2 = ti;
-        t2.advance(dq, dr);
-        t2.advance(dq, dr);
-        v_stage(args, xraw, lbuf + ((it + 2) & 3) * MLP2_LAB, (int64_t)(tile + 2 * G) * T, t2, wave, lane, Cin);
-      }
-#pragma unroll
-      for (int cb = 0; cb < 6; ++cb) {
-        const int off = vt_off(16 * cb + lc, lg);
-        const SplitD xd = {*(const h8*)(timg + off), *(const h8*)(timg + V_FRAGT + off), *(const h8*)(timg + 2 * V_FRAGT + off)};
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) dw[cb][nb] = mfma3_16(xd, dsp[nb], dw[cb][nb]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    VSTAMP(7);
-  }
-
-#ifdef MLP2_STAMPS
-  if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4))
-    printf("VSTAMP w%d fwdmfma %u act+part %u split %u bar %u stage %u head %u brows %u bmfma %u\n", wave, vph[0],
-           vph[1], vph[2], vph[3], vph[4], vph[5], vph[6], vph[7]);
-#endif
-  // ---- flush this workgroup's partial gradients + loss sums ----
-#ifdef MLP2_DIAG_BAR_FLUSH
-  __syncthreads();
-#endif
-  const int slab = prog[H_SLAB];
-  const int npt = prog[H_NPARAMS_TRAIN];
-  float* ws = args.ws + (size_t)blockIdx.x * slab;
-  const float sc = args.inv_count;
-  bool bad_flush = false;
-  {
-    float chk = 0.f;
-#pragma unroll
-    for (int nb = 0; nb < 3; ++nb) {
-      const int n = n0 + 16 * nb;
-      const float s2f = colt[n * 4 + 2];
-#pragma unroll
-      for (int cb = 0; cb < 6; ++cb) {
-        chk += (dw[cb][nb][0] + dw[cb][nb][1]) + (dw[cb][nb][2] + dw[cb][nb][3]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int k = 16 * cb + 4 * lg + i;
-          if (k < Cin && n < F) ws[o[O_W] + (size_t)k * F + n] = dw[cb][nb][i] * (sc * (SPLIT_INV_C / s2f));
-        }
-      }
-      const f32x4 gs = *(const f32x4*)(gme + 64 * nb);
-      float tb = gs.w + __shfl_xor(gs.w, 16, 64);
-      tb += xor32(tb);
-      tb *= 1.f / s2f;  // the db1 sums carry the unit's power-of-two scale s2 (exact)
-      float t2[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        t2[j] = gs[j] + __shfl_xor(gs[j], 16, 64);
-        t2[j] += xor32(t2[j]);
-      }
-      if (lg == 0 && n < F) {
-        if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
-      }
-    }
-    bad_flush = !(fabsf(chk) <= 3.0e38f);
-  }
-  if (bad || bad_flush) {
-    __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // which check fired (forward sum: 1, dW1 flush: 2), read back by hpe_guard_peek (race screens)
-    __hip_atomic_fetch_or(args.guard + HPE_GUARD_RING, (bad ? 1 : 0) | (bad_flush ? 2 : 0), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (wave == 0) {
-    const f32x4 h0 = half == 0 ? *(const f32x4*)(hac + l32 * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const float h1 = half == 0 ? hac[l32 * 8 + 4] : 0.f;
-    const float a = wave_sum(h0.x), b = wave_sum(h0.y);
-    const float d0 = wave_sum(h0.z), d1 = wave_sum(h0.w), d2 = wave_sum(h1);
-    if (lane == 0) {
-      ws[npt] = a;
-      ws[npt + 1] = b;
-      if (o[O_AUX1] >= 0) {
-        ws[o[O_AUX1] + 0] = d0 * sc;
-        ws[o[O_AUX1] + 1] = d1 * sc;
-        ws[o[O_AUX1] + 2] = d2 * sc;
-      }
-    }
-  }
-}
-
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
@@ -1766,53 +710,8 @@ static mlp2_fn pick_act(int act, int act2) {
   return mlp2_kernel<KH, -1, DROP, NWM, SPLIT>;
 }
 
-// the one-barrier 12-wave kernel (HPE_MLP2_1BAR=1): measured slower than mlp2_kernel so far
-static bool mlp2_one_barrier() {
-  const char* e = getenv("HPE_MLP2_1BAR");
-  return e && e[0] == '1';
-}
-template <int KH, bool DROP>
-static mlp2_fn pick_w(int act, int act2) {
-  if (act2 != ACT_LINEAR) return mlp2w_kernel<KH, -1, DROP>;
-  if (act == ACT_TANH) return mlp2w_kernel<KH, ACT_TANH, DROP>;
-  if (act == ACT_SOFTSIGN) return mlp2w_kernel<KH, ACT_SOFTSIGN, DROP>;
-  return mlp2w_kernel<KH, -1, DROP>;
-}
-
-// the 8-wave 16x16x32 kernel (mlp2v_kernel): OPT-IN (HPE_MLP2_V=1) since round 4 — its gradient is
-// not reproducible launch to launch (DESIGN.md, mlp2v open issue: rare dropped dW2 terms, a 1e-5
-// deviation of the configs[3] gradient in some processes, wrong dW2 with dropout on 8x8 maps); the
-// default is the 12-wave mlp2_kernel, which no screen has caught
-static bool mlp2_v_enabled() {
-  const char* e = getenv("HPE_MLP2_V");
-  return e && e[0] == '1';
-}
-// mlp2v only where every workgroup walks at least two tiles: at one tile per workgroup (launches of
-// fewer than 2 x grid tiles) its dW2 accumulation is not reproducible (DESIGN.md, mlp2v open
-// issue: one row's term of one 16-lane group dropped in rare launches, and with SpatialDropout on
-// the tanh instantiation wrong dW2 in most launches); those launches run the 12-wave mlp2_kernel
-static bool use_v(const int* w, const Args& a, int grid) {
-  const int* o = w + w[H_OPS_OFF];
-  const int ncb = o[O_MODE];
-  const int64_t ntiles = (a.nrows + 31) / 32;
-  return mlp2_v_enabled() && !mlp2_one_barrier() && w[H_MODE] == MODE_TRAIN && a.P >= 32 &&
-         ncb > 4 && ncb <= MLP2_MAXW && o[O_K] <= 96 && ntiles >= 2 * (int64_t)grid &&
-         o[O_EDROP] < 0 && o[O_TBASE] < 0;  // no SpatialDropout on either layer
-}
-template <bool DROP>
-static mlp2_fn pick_v(int act, int act2) {
-  if (act2 != ACT_LINEAR) return mlp2v_kernel<-1, DROP>;
-  if (act == ACT_TANH) return mlp2v_kernel<ACT_TANH, DROP>;
-  if (act == ACT_SOFTSIGN) return mlp2v_kernel<ACT_SOFTSIGN, DROP>;
-  return mlp2v_kernel<-1, DROP>;
-}
-
 template <bool DROP, bool SPLIT>
 static mlp2_fn pick_d(int kh, int act, int act2, int ncb) {
-  if (SPLIT && ncb > 4 && mlp2_one_barrier()) {  // the one-barrier 12-wave kernel
-    if (kh == 44) return pick_w<44, DROP>(act, act2);
-    if (kh == 48) return pick_w<48, DROP>(act, act2);
-  }
   if (ncb <= 4) {
     if (kh == 44) return pick_act<44, DROP, 4, SPLIT>(act, act2);  // 88-channel BlazeFace tap (Model-88)
     if (kh == 48) return pick_act<48, DROP, 4, SPLIT>(act, act2);  // 96-channel tap (Model-96)
@@ -1851,7 +750,6 @@ static void geom(const int* w, int& kh, int& rbw, int& ncb, int& lds_bytes, int&
 static int lds_split(const int* w) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
-  if (ncb > 4 && mlp2_one_barrier()) return w_lds_floats(ncb) * 4;
   return lds;
 }
 
@@ -1876,20 +774,15 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
   if (hpe_exact_fp32() || !a.guard) {
     Args e = a;
     e.guard = nullptr;
-    hpe_tev_begin(s);
+    const int tv = hpe_tev_begin(s);
     const int rc = launch_k(pick(w), ncb, lds, e, grid, s);
-    hpe_tev_end(s);
+    hpe_tev_end(s, tv);
     return rc;
   }
-  hpe_tev_begin(s);
-  if (use_v(w, a, grid)) {
-    const int* o = w + w[H_OPS_OFF];
-    const mlp2_fn kv = o[O_EDROP] >= 0 ? pick_v<true>(act, o[O_AUX2]) : pick_v<false>(act, o[O_AUX2]);
-    if (launch_k(kv, V_NW, v_lds_floats() * 4, a, grid, s)) return 2;
-  } else if (launch_k(pick(w, true), ncb, lds_split(w), a, grid, s)) {
-    return 2;
-  }
-  hpe_tev_end(s);
+  const int tv = hpe_tev_begin(s);
+  const int rc = launch_k(pick(w, true), ncb, lds_split(w), a, grid, s);
+  hpe_tev_end(s, tv);
+  if (rc) return rc;
   if (split_only()) return 0;
   // inputs the caller bounds below the data-side range: the guard cannot fire (finite weights are
   // scaled into range), so the exact twin's early-exit launch is not queued
@@ -1911,17 +804,12 @@ static int per_cu_of(mlp2_fn k, int ncb, int lds) {
 }
 
 // resident workgroups per CU of this object's kernels for program w: the smaller of the split and
-// exact instantiations (and of mlp2v_kernel for the training launches that may run it)
+// exact instantiations
 static int cap_per_cu(const int* w) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
   const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds_split(w));
-  int m = a < b ? a : b;
-  if (ncb > 4) {  // training launches may run mlp2v_kernel (LDS-bound to one workgroup per CU)
-    const int c = per_cu_of(pick_v<false>(ACT_TANH, ACT_LINEAR), V_NW, v_lds_floats() * 4);
-    m = m < c ? m : c;
-  }
-  return m;
+  return a < b ? a : b;
 }
 }  // namespace MLP2_NS
 

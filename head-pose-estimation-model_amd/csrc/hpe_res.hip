@@ -44,17 +44,7 @@
 #define RES_L_MISC (RES_L_RED + 4 * (RES_MAXP + 4))   // 4 flat partial-gradient copies
 #define RES_LDS_FLOATS (RES_L_MISC + 64)
 #define RES_LDS_BYTES (RES_LDS_FLOATS * 4)
-// the wide two-layer kernels (create_model 88 -> 64 -> 3: 5,891 parameters): more parameters in
-// LDS; the fit kernel's optimizer moments stay in the caller's global m / v (L2-resident, read and
-// written once per step by the optimizer, WIDE_MV per thread) instead of LDS
-#define WIDE_MAXP 6144
-#define WIDE_MV (WIDE_MAXP / (RES_NW * 64))
-#define WIDE_L_PRM 0
-#define WIDE_L_SCR (WIDE_L_PRM + WIDE_MAXP)
-#define WIDE_L_RED (WIDE_L_SCR + RES_NW * RES_SCR)
-#define WIDE_L_MISC (WIDE_L_RED + 4 * (WIDE_MAXP + 4))
-#define WIDE_LDS_BYTES ((WIDE_L_MISC + 64) * 4)
-static_assert(RES_LDS_BYTES <= 160 * 1024 && WIDE_LDS_BYTES <= 160 * 1024, "res LDS");
+static_assert(RES_LDS_BYTES <= 160 * 1024, "res LDS");
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -471,201 +461,6 @@ __device__ __forceinline__ float res_sum4(const float* cp, int stride, int i) {
   return (cp[i] + cp[stride + i]) + (cp[2 * stride + i] + cp[3 * stride + i]);
 }
 
-// ================================================================================================
-// The same machinery for the 2-layer create_model family with a narrow hidden layer (train_88.py
-// :66-140 create_model: 88 -> 64 softsign -> 3, configs[2]'s Model-88 training at batch 512, and any
-// F <= 64 multiple of 16): x -> dense F (act, dropout) -> dense 3 (act, dropout).  The hidden layer
-// is FB = F / 16 R-layout blocks; the output layer's K runs over them.  Used for P = 1 training
-// launches and the whole-epoch kernel (P > 1 launches keep mlp2_kernel, which tiles 32 rows x all
-// units per workgroup for the large-map lines).
-// ================================================================================================
-template <int KS, int FB>
-struct WideState {
-  f4 acc0[(4 * KS + 15) / 16][FB];   // dW0[16 b + 4g + i][16 bn + c]
-  f4 acco[FB];                       // dWo[16 bk + 4g + i][c]
-  float db0[FB], dbo;
-  float sse, sae;
-};
-
-template <int KS, int FB>
-__device__ __forceinline__ void wide_zero(WideState<KS, FB>& S) {
-#pragma unroll
-  for (int b = 0; b < (4 * KS + 15) / 16; ++b)
-#pragma unroll
-    for (int j = 0; j < FB; ++j) S.acc0[b][j] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < FB; ++j) {
-    S.acco[j] = f4{0.f, 0.f, 0.f, 0.f};
-    S.db0[j] = 0.f;
-  }
-  S.dbo = S.sse = S.sae = 0.f;
-}
-
-// layer descriptors: HA >= 0 (create_model's canonical packing: W0 [C_in][F], b0, W1 [F][3], b1;
-// the hidden activation HA, the output linear) or the program's runtime words
-template <int KS, int FB, int HA>
-__device__ __forceinline__ void wide_desc(const int* lt, LD& e0, LD& eo) {
-  const int* t[2] = {lt, lt + RL_WORDS};
-  LD* d[2] = {&e0, &eo};
-#pragma unroll
-  for (int l = 0; l < 2; ++l) {
-    const int* e = t[l];
-    if (HA >= 0) {
-      d[l]->K = l == 0 ? 4 * KS : 16 * FB;
-      d[l]->N = l == 0 ? 16 * FB : 3;
-      d[l]->wo = l == 0 ? 0 : 4 * KS * 16 * FB + 16 * FB;
-      d[l]->bo = d[l]->wo + d[l]->K * d[l]->N;
-      d[l]->act = l == 0 ? HA : ACT_LINEAR;
-    } else {
-      d[l]->K = e[RL_K];
-      d[l]->N = e[RL_N];
-      d[l]->wo = e[RL_W];
-      d[l]->bo = e[RL_B];
-      d[l]->act = e[RL_ACT];
-    }
-    d[l]->drop = e[RL_DROP];
-    d[l]->thr = (uint32_t)e[RL_THR];
-    d[l]->ik = 1.f / __int_as_float(e[RL_KEEP]);
-  }
-}
-
-template <int KS, int FB>
-__device__ __forceinline__ void wide_block(WideState<KS, FB>& S, const LD& e0, const LD& eo, const float* prm,
-                                           const float* __restrict__ x, const float* __restrict__ ytrue,
-                                           const RowMap& rm, int64_t R0, uint64_t seed, float inv_count, float* scr,
-                                           int g, int c) {
-  constexpr int CIN = 4 * KS, NXB = (CIN + 15) / 16;
-  const int64_t Rc = R0 + c;
-  const bool valid = Rc < rm.nrows;
-  const int64_t Rl = valid ? Rc : rm.nrows - 1;
-  const uint64_t dimg = rm.dimg(Rl);
-  // ---- hidden layer: FB output blocks, K = C_in from HBM
-  f4 a0[FB], h[FB];
-  uint32_t m0[FB];
-  {
-    const float* xp = x + rm.src(Rl) * CIN + KS * g;
-    float xr[KS];
-#pragma unroll
-    for (int s = 0; s < KS; s += 2) {
-      const float2 v = *(const float2*)(xp + s);
-      xr[s] = v.x;
-      xr[s + 1] = v.y;
-    }
-    const float* w0 = prm + e0.wo + KS * g * e0.N + c;   // W0[KS g + s][16 bn + c]
-#pragma unroll
-    for (int bn = 0; bn < FB; ++bn) {
-      f4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) z = mfma4(w0[s * e0.N + 16 * bn], xr[s], z);
-      h[bn] = res_epi(z, prm, e0, g, seed, dimg, a0[bn], m0[bn], 16 * bn);
-    }
-  }
-  float xt[NXB][4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int64_t R = min(R0 + 4 * g + s, rm.nrows - 1);
-    const float* xp = x + rm.src(R) * CIN;
-#pragma unroll
-    for (int b = 0; b < NXB; ++b) {
-      const int ch = 16 * b + c;
-      const float v = xp[min(ch, CIN - 1)];
-      xt[b][s] = ch < CIN ? v : 0.f;
-    }
-  }
-  // ---- output layer: K = F over the FB blocks
-  f4 zo = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int bk = 0; bk < FB; ++bk) zo = res_fwd16(prm, eo, g, c, h[bk], 16 * bk, 0, zo);
-  f4 ao;
-  uint32_t mo;
-  const f4 out = res_epi(zo, prm, eo, g, seed, dimg, ao, mo);
-  f4 dout = {0.f, 0.f, 0.f, 0.f};
-  if (g == 0 && valid) {
-    const float* yl = ytrue + rm.label(Rl) * 3;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float err = out[i] - yl[i];
-      S.sse = fmaf(err, err, S.sse);
-      S.sae += fabsf(err);
-      dout[i] = 2.f * err * inv_count;
-    }
-  }
-  // ---- backward
-  const f4 dz = res_epi_bwd(dout, ao, eo, mo);
-  float dt[4];
-  res_to_t(scr + 320, dz, g, c, dt);
-  S.dbo += (dt[0] + dt[1]) + (dt[2] + dt[3]);
-#pragma unroll
-  for (int bk = 0; bk < FB; ++bk) {
-    float at[4];
-    res_to_t(scr, h[bk], g, c, at);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) S.acco[bk] = mfma4(at[s], dt[s], S.acco[bk]);
-  }
-#pragma unroll
-  for (int bk = 0; bk < FB; ++bk) {
-    const f4 dz1 = res_epi_bwd(res_bwd16(prm, eo, g, c, dz, 16 * bk, 0), a0[bk], e0, m0[bk]);
-    float d1[4];
-    res_to_t(scr, dz1, g, c, d1);
-#pragma unroll
-    for (int b = 0; b < NXB; ++b)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) S.acc0[b][bk] = mfma4(xt[b][s], d1[s], S.acc0[b][bk]);
-    S.db0[bk] += (d1[0] + d1[1]) + (d1[2] + d1[3]);
-  }
-}
-
-template <int KS, int FB, bool ADD>
-__device__ __forceinline__ void wide_flat(const WideState<KS, FB>& S, const LD& e0, const LD& eo, float* out, int npt,
-                                          int g, int c, int lane) {
-  constexpr int CIN = 4 * KS, NXB = (CIN + 15) / 16;
-#define RES_PUT(idx, v) do { float* p_ = out + (idx); *p_ = ADD ? *p_ + (v) : (v); } while (0)
-#pragma unroll
-  for (int b = 0; b < NXB; ++b)
-#pragma unroll
-    for (int bn = 0; bn < FB; ++bn)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int in = 16 * b + 4 * g + i, n = 16 * bn + c;
-        if (in < CIN && n < e0.N) RES_PUT(e0.wo + in * e0.N + n, S.acc0[b][bn][i]);
-      }
-#pragma unroll
-  for (int bk = 0; bk < FB; ++bk)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int in = 16 * bk + 4 * g + i;
-      if (in < eo.K && c < eo.N) RES_PUT(eo.wo + in * eo.N + c, S.acco[bk][i]);
-    }
-#pragma unroll
-  for (int bn = 0; bn < FB; ++bn) {
-    float v = S.db0[bn];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (g == 0 && e0.bo >= 0 && 16 * bn + c < e0.N) RES_PUT(e0.bo + 16 * bn + c, v);
-  }
-  {
-    float v = S.dbo;
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (g == 0 && eo.bo >= 0 && c < eo.N) RES_PUT(eo.bo + c, v);
-  }
-  const float a = wave_sum(S.sse), b = wave_sum(S.sae);
-  if (lane == 0) {
-    RES_PUT(npt, a);
-    RES_PUT(npt + 1, b);
-  }
-#undef RES_PUT
-}
-
-template <int KS, int FB>
-__device__ __forceinline__ void wide_reduce(const WideState<KS, FB>& S, const LD& e0, const LD& eo, float* cp, int npt,
-                                            int stride, int wave, int g, int c, int lane) {
-  if (wave >= 4) wide_flat<KS, FB, false>(S, e0, eo, cp + (wave - 4) * stride, npt, g, c, lane);
-  __syncthreads();
-  if (wave < 4) wide_flat<KS, FB, true>(S, e0, eo, cp + wave * stride, npt, g, c, lane);
-  __syncthreads();
-}
-
 // The file is compiled five times (csrc/Makefile): RES_PART 88 / 96 with RES_FAST 0 / 1 instantiate
 // the kernels of one input width and activation set, RES_PART 0 the host dispatch (the kernel
 // instantiations take minutes to compile).
@@ -741,45 +536,18 @@ __device__ __forceinline__ float res_opt_one(const ResFitArgs& a, float alpha, f
   return wi - alpha * (mi / (vi + a.eps));
 }
 
-// GM: the optimizer moments are the caller's global a.m / a.v (all of a thread's loads issued
-// before the first use), not LDS mom / vel
-template <bool GM>
 __device__ __forceinline__ void res_opt_step(const ResFitArgs& a, float* prm, float* mom, float* vel, const float* cp,
                                              int stride, int npt, int s, float* misc, int tid, int lane, int wave) {
   const float alpha = a.alpha[s];
   float reg = 0.f;
-  if (GM) {
-    float mr[WIDE_MV], vr[WIDE_MV];
-    const bool mv = a.kind != HPE_OPT_SGD;
-#pragma unroll
-    for (int k = 0; k < WIDE_MV; ++k) {
-      const int i = tid + k * RES_NW * 64;
-      mr[k] = mv && i < npt ? a.m[i] : 0.f;
-      vr[k] = mv && i < npt ? a.v[i] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < WIDE_MV; ++k) {
-      const int i = tid + k * RES_NW * 64;
-      if (i < npt) {
-        const float wi = prm[i], c2 = a.l2[i];
-        reg = fmaf(c2 * wi, wi, reg);
-        prm[i] = res_opt_one(a, alpha, wi, c2, res_sum4(cp, stride, i), mr[k], vr[k]);
-        if (mv) {
-          a.m[i] = mr[k];
-          a.v[i] = vr[k];
-        }
-      }
-    }
-  } else {
-    for (int i = tid; i < npt; i += RES_NW * 64) {
-      const float wi = prm[i], c2 = a.l2[i];
-      reg = fmaf(c2 * wi, wi, reg);
-      float mi = mom[i], vi = vel[i];
-      prm[i] = res_opt_one(a, alpha, wi, c2, res_sum4(cp, stride, i), mi, vi);
-      if (a.kind != HPE_OPT_SGD) {
-        mom[i] = mi;
-        vel[i] = vi;
-      }
+  for (int i = tid; i < npt; i += RES_NW * 64) {
+    const float wi = prm[i], c2 = a.l2[i];
+    reg = fmaf(c2 * wi, wi, reg);
+    float mi = mom[i], vi = vel[i];
+    prm[i] = res_opt_one(a, alpha, wi, c2, res_sum4(cp, stride, i), mi, vi);
+    if (a.kind != HPE_OPT_SGD) {
+      mom[i] = mi;
+      vel[i] = vi;
     }
   }
   reg = wave_sum(reg);
@@ -839,7 +607,7 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
       res_block(S, D, prm, a.x, a.ytrue, rm, (int64_t)blk * RES_T, seed, inv, scr, g, c);
     res_reduce(S, D, cp, npt, stride, wave, g, c, lane);
     RSTAMP(4);
-    res_opt_step<false>(a, prm, mom, vel, cp, stride, npt, s, misc, tid, lane, wave);
+    res_opt_step(a, prm, mom, vel, cp, stride, npt, s, misc, tid, lane, wave);
     RSTAMP(5);
   }
 #ifdef RES_STAMPS
@@ -857,78 +625,6 @@ __global__ void __launch_bounds__(RES_NW * 64) res_fit_kernel(ResFitArgs a) {
       a.m[i] = mom[i];
       a.v[i] = vel[i];
     }
-  }
-}
-
-// ---- the wide two-layer kernels: same launch shapes, LDS layout and reduction order -----------------
-template <int KS, int FB, int HA>
-__global__ void __launch_bounds__(RES_NW * 64) wide_train_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int* prog = a.prog;
-  const int* o = prog + prog[H_OPS_OFF];
-  const int* lt = prog + o[O_AUX0];
-  const int npt = prog[H_NPARAMS_TRAIN];
-  const int stride = (npt + 4 + 3) & ~3;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  float* prm = lds + WIDE_L_PRM;
-  float* scr = lds + WIDE_L_SCR + wave * RES_SCR;
-  float* cp = lds + WIDE_L_RED;
-  for (int i = threadIdx.x; i < npt; i += RES_NW * 64) prm[i] = a.params[i];
-  LD e0, eo;
-  wide_desc<KS, FB, HA>(lt, e0, eo);
-  __syncthreads();
-  WideState<KS, FB> S;
-  wide_zero(S);
-  RowMap rm = {a.idx, nullptr, 0, a.nrows, a.img_off, a.P, false};
-  const int64_t nblk = (a.nrows + RES_T - 1) / RES_T;
-  for (int64_t blk = (int64_t)blockIdx.x * RES_NW + wave; blk < nblk; blk += (int64_t)gridDim.x * RES_NW)
-    wide_block(S, e0, eo, prm, a.x, a.ytrue, rm, blk * RES_T, a.seed, a.inv_count, scr, g, c);
-  wide_reduce(S, e0, eo, cp, npt, stride, wave, g, c, lane);
-  float* ws = a.ws + (size_t)blockIdx.x * prog[H_SLAB];
-  for (int i = threadIdx.x; i < npt + 2; i += RES_NW * 64) ws[i] = res_sum4(cp, stride, i);
-  if (threadIdx.x < 2) ws[npt + 2 + threadIdx.x] = 0.f;
-}
-
-template <int KS, int FB, int HA>
-__global__ void __launch_bounds__(RES_NW * 64) wide_fit_kernel(ResFitArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int* prog = a.prog;
-  const int* o = prog + prog[H_OPS_OFF];
-  const int* lt = prog + o[O_AUX0];
-  const int npt = prog[H_NPARAMS_TRAIN];
-  const int stride = (npt + 4 + 3) & ~3;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int tid = threadIdx.x;
-  float* prm = lds + WIDE_L_PRM;
-  float* scr = lds + WIDE_L_SCR + wave * RES_SCR;
-  float* cp = lds + WIDE_L_RED;
-  float* misc = lds + WIDE_L_MISC;
-  for (int i = tid; i < npt; i += RES_NW * 64) prm[i] = a.params[i];
-  if (tid == 0) a.flags[1] = 0;
-  LD e0, eo;
-  wide_desc<KS, FB, HA>(lt, e0, eo);
-  __syncthreads();
-  WideState<KS, FB> S;
-  for (int s = 0; s < a.steps; ++s) {
-    const int64_t base = (int64_t)s * a.bs;
-    const int nb = (int)min((int64_t)a.bs, (int64_t)a.n - base);
-    wide_zero(S);
-    RowMap rm = {nullptr, a.perm, base, nb, 0, 1, true};
-    const uint64_t seed = a.seed_base + (uint64_t)(a.iter0 + 1 + s);
-    const float inv = 1.f / (float)(nb * 3);
-    const int nblk = (nb + RES_T - 1) / RES_T;
-    for (int blk = wave; blk < nblk; blk += RES_NW)
-      wide_block(S, e0, eo, prm, a.x, a.ytrue, rm, (int64_t)blk * RES_T, seed, inv, scr, g, c);
-    wide_reduce(S, e0, eo, cp, npt, stride, wave, g, c, lane);
-    res_opt_step<true>(a, prm, nullptr, nullptr, cp, stride, npt, s, misc, tid, lane, wave);
-  }
-  for (int i = tid; i < npt; i += RES_NW * 64) {
-    const float w = prm[i];
-    a.params[i] = w;
-    const int tp = a.tpos[i];
-    if (tp >= 0) a.params_t[tp] = w;
   }
 }
 
@@ -953,41 +649,23 @@ static void res_pick_nb(int nb, res_train_fn* t, res_fit_fn* f) {
 }
 #define RES_FNS_NAME3(n, f) res_fns_##n##_##f
 #define RES_FNS_NAME(n, f) RES_FNS_NAME3(n, f)
-// nb > 0: a residual stack of nb blocks (bot: with the bottleneck); nb = 0: the wide two-layer net
-// of hidden width 16 * fb
-void RES_FNS_NAME(RES_PART, RES_FAST)(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f) {
-  if (nb == 0) {
-    switch (fb) {
-      case 1: *t = wide_train_kernel<RES_PART / 4, 1, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 1, RES_HA>; break;
-      case 2: *t = wide_train_kernel<RES_PART / 4, 2, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 2, RES_HA>; break;
-      case 3: *t = wide_train_kernel<RES_PART / 4, 3, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 3, RES_HA>; break;
-      case 4: *t = wide_train_kernel<RES_PART / 4, 4, RES_HA>; *f = wide_fit_kernel<RES_PART / 4, 4, RES_HA>; break;
-      default: break;
-    }
-    return;
-  }
+// a residual stack of nb blocks (bot: with the bottleneck)
+void RES_FNS_NAME(RES_PART, RES_FAST)(int nb, bool bot, res_train_fn* t, res_fit_fn* f) {
   if (bot) res_pick_nb<RES_PART / 4, true>(nb, t, f);
   else res_pick_nb<RES_PART / 4, false>(nb, t, f);
 }
 #else
-void res_fns_88_0(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
-void res_fns_88_1(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
-void res_fns_96_0(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
-void res_fns_96_1(int nb, bool bot, int fb, res_train_fn* t, res_fit_fn* f);
+void res_fns_88_0(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
+void res_fns_88_1(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
+void res_fns_96_0(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
+void res_fns_96_1(int nb, bool bot, res_train_fn* t, res_fit_fn* f);
 
 // the compile-time-activation kernels: every hidden dense softsign, the post-add activation relu,
 // the output linear (create_model_complex, Model-88/attention_model.py:97-169)
 static bool res_fast(const int* w) {
   const int* o = w + w[H_OPS_OFF];
   const int* lt = w + o[O_AUX0];
-  const int L = o[O_AUX1], cin = o[O_K], nb = o[O_AUX3], bot = o[O_FLAGS], F = o[O_N];
-  if (nb == 0) {   // wide two-layer net: W0 [C_in][F], b0, W1 [F][3], b1; softsign, linear
-    const int* e0 = lt;
-    const int* e1 = lt + RL_WORDS;
-    return L == 2 && e0[RL_W] == 0 && e0[RL_B] == cin * F && e1[RL_W] == cin * F + F && e1[RL_B] == cin * F + F + 3 * F &&
-           e0[RL_K] == cin && e0[RL_N] == F && e1[RL_K] == F && e1[RL_N] == 3 && e0[RL_ACT] == ACT_SOFTSIGN &&
-           e1[RL_ACT] == ACT_LINEAR && w[H_NPARAMS_TRAIN] == cin * F + F + 3 * F + 3;
-  }
+  const int L = o[O_AUX1], cin = o[O_K], nb = o[O_AUX3], bot = o[O_FLAGS];
   if (o[O_MODE] != ACT_RELU || (bot != 0 && bot != 8)) return false;
   int off = 0;
   for (int l = 0; l < L; ++l) {
@@ -1008,19 +686,16 @@ static bool res_pick(const int* w, res_train_fn* t, res_fit_fn* f) {
   if (o[O_TYPE] != OP_RES) return false;
   const int cin = o[O_K], nb = o[O_AUX3], F = o[O_N];
   const bool bot = o[O_FLAGS] > 0;
-  if (nb > 0 && (F != 16 || o[O_AUX1] != 2 * nb + 2 + (bot ? 1 : 0))) return false;
-  if (nb == 0 && (F % 16 || F < 16 || F > 64 || bot || o[O_AUX1] != 2)) return false;
+  if (nb <= 0 || F != 16 || o[O_AUX1] != 2 * nb + 2 + (bot ? 1 : 0)) return false;
   const bool fast = res_fast(w);
-  if (cin == 88) (fast ? res_fns_88_1 : res_fns_88_0)(nb, bot, F / 16, t, f);
-  else if (cin == 96) (fast ? res_fns_96_1 : res_fns_96_0)(nb, bot, F / 16, t, f);
+  if (cin == 88) (fast ? res_fns_88_1 : res_fns_88_0)(nb, bot, t, f);
+  else if (cin == 96) (fast ? res_fns_96_1 : res_fns_96_0)(nb, bot, t, f);
   return *t != nullptr;
 }
 int res_supported(const int* w) {
   res_train_fn t;
   res_fit_fn f;
-  const int* o = w + w[H_OPS_OFF];
-  const int maxp = o[O_TYPE] == OP_RES && o[O_AUX3] == 0 ? WIDE_MAXP : RES_MAXP;
-  return w[H_MODE] == MODE_TRAIN && w[H_NPARAMS_TRAIN] <= maxp && res_pick(w, &t, &f) ? 1 : 0;
+  return w[H_MODE] == MODE_TRAIN && w[H_NPARAMS_TRAIN] <= RES_MAXP && res_pick(w, &t, &f) ? 1 : 0;
 }
 
 int res_grid_cap(int n_cu) { return n_cu; }
@@ -1029,11 +704,11 @@ int res_launch(const int* w, const Args& a, int grid, hipStream_t s) {
   res_train_fn t;
   res_fit_fn f;
   if (!res_pick(w, &t, &f)) return 2;
-  const int lds = w[w[H_OPS_OFF] + O_AUX3] == 0 ? WIDE_LDS_BYTES : RES_LDS_BYTES;
+  const int lds = RES_LDS_BYTES;
   hipFuncSetAttribute((const void*)t, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hpe_tev_begin(s);
+  const int tv = hpe_tev_begin(s);
   hipLaunchKernelGGL(t, dim3(grid), dim3(RES_NW * 64), lds, s, a);
-  hpe_tev_end(s);
+  hpe_tev_end(s, tv);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -1054,11 +729,11 @@ int res_fit_launch(const int* w, const int* dwords, float* params, float* params
   a.alpha = alpha; a.seed_base = seed_base; a.iter0 = iter0;
   a.stats = stats; a.stats_stride = stats_stride;
   a.flags = (int*)workspace;
-  const int lds = w[w[H_OPS_OFF] + O_AUX3] == 0 ? WIDE_LDS_BYTES : RES_LDS_BYTES;
+  const int lds = RES_LDS_BYTES;
   hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hpe_tev_begin(s);
+  const int tv = hpe_tev_begin(s);
   hipLaunchKernelGGL(f, dim3(1), dim3(RES_NW * 64), lds, s, a);
-  hpe_tev_end(s);
+  hpe_tev_end(s, tv);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 #endif

@@ -19,6 +19,7 @@
 // LayerNormalization (attention_model.py:57,61), MSE loss + MAE metric (train_96.py:51-52), the
 // autodiff of Keras' fit (train_96.py:175).  Optimizers: Keras legacy SGD/Adam/Adamax.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <math.h>
 #include <stdlib.h>
 #include <stdarg.h>
@@ -1028,14 +1029,25 @@ bool hpe_exact_fp32() {
 // a pool of event pairs recorded around each launch's dominant kernel while timing is on; the
 // events are created up front by hpe_kernel_timing, so recording never allocates
 static std::vector<hipEvent_t> g_tev;
-static int g_tev_cap = 0, g_tev_n = 0;
+static int g_tev_cap = 0;
+static std::atomic<int> g_tev_n{0};
 static bool g_tev_on = false;
 
-void hpe_tev_begin(hipStream_t s) {
-  if (g_tev_on && g_tev_n < g_tev_cap) hipEventRecord(g_tev[2 * g_tev_n], s);
+// reserves the next event pair (launch() may run on several host threads): the slot to pass to
+// hpe_tev_end, -1 when timing is off or the pool is full
+int hpe_tev_begin(hipStream_t s) {
+  if (!g_tev_on) return -1;
+  const int slot = g_tev_n.fetch_add(1, std::memory_order_relaxed);
+  if (slot >= g_tev_cap) {
+    g_tev_n.store(g_tev_cap, std::memory_order_relaxed);
+    return -1;
+  }
+  hipEventRecord(g_tev[2 * slot], s);
+  return slot;
 }
-void hpe_tev_end(hipStream_t s) {
-  if (g_tev_on && g_tev_n < g_tev_cap) hipEventRecord(g_tev[2 * g_tev_n++ + 1], s);
+// called on every path after hpe_tev_begin, failed launches included, so no slot stays half-recorded
+void hpe_tev_end(hipStream_t s, int slot) {
+  if (slot >= 0) hipEventRecord(g_tev[2 * slot + 1], s);
 }
 
 extern "C" int hpe_kernel_timing(int32_t capacity) {
@@ -1054,7 +1066,8 @@ extern "C" int hpe_kernel_timing(int32_t capacity) {
 
 extern "C" int hpe_kernel_times(float* ms, int32_t max) {
   if (!ms && max > 0) return fail(HPE_EINVAL, "hpe_kernel_times: null argument");
-  const int n = g_tev_n < max ? g_tev_n : max;
+  const int done = g_tev_n.load(std::memory_order_relaxed);
+  const int n = done < max ? done : max;
   for (int i = 0; i < n; ++i) {
     HIPCHK(hipEventSynchronize(g_tev[2 * i + 1]));
     HIPCHK(hipEventElapsedTime(&ms[i], g_tev[2 * i], g_tev[2 * i + 1]));
@@ -1303,23 +1316,26 @@ static int launch(const hpe_program* p, Args a, int64_t nrows, hipStream_t s) {
                        (const int*)p->split_tab, a.params, a.params_t, p->wsplit);
     HIPCHK(hipGetLastError());
     a.wsplit = p->wsplit;
-    hpe_tev_begin(s);
+    const int tv = hpe_tev_begin(s);
     hipLaunchKernelGGL(ks, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
-    HIPCHK(hipGetLastError());
-    hpe_tev_end(s);
+    const hipError_t le = hipGetLastError();
+    hpe_tev_end(s, tv);
+    HIPCHK(le);
     hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
     HIPCHK(hipGetLastError());
     return HPE_OK;
   }
   a.guard = nullptr;  // no split launch ahead: the kernel runs unconditionally
   const int npass = p->hdr[H_MODE] == MODE_TRAIN && p->hdr[H_NPASS] > 1 ? p->hdr[H_NPASS] : 1;
-  hpe_tev_begin(s);
-  for (int pass = 0; pass < npass; ++pass) {
+  const int tv = hpe_tev_begin(s);
+  hipError_t le = hipSuccess;
+  for (int pass = 0; pass < npass && le == hipSuccess; ++pass) {
     a.pass = pass;
     hipLaunchKernelGGL(k, dim3(grid), dim3(p->hdr[H_NW] * 64), lds_bytes_of(p->hdr), s, a);
-    HIPCHK(hipGetLastError());
+    le = hipGetLastError();
   }
-  hpe_tev_end(s);
+  hpe_tev_end(s, tv);
+  HIPCHK(le);
   return HPE_OK;
 }
 
@@ -1445,9 +1461,13 @@ extern "C" int hpe_fit_steps(const hpe_program* p, float* params, float* params_
                              int32_t stats_stride, void* stream) {
   if (!p || !params || !x || !ytrue || !perm || !ws || !grad || !l2 || !tpos || !stats)
     return fail(HPE_EINVAL, "hpe_fit_steps: null argument");
-  if (n <= 0 || batch <= 0 || P <= 0 || iter0 < 0 || stats_stride < 2)
+  if (n <= 0 || batch <= 0 || P <= 0 || iter0 < 0)
     return fail(HPE_EINVAL, "hpe_fit_steps: bad shape n=%lld batch=%d P=%d", (long long)n, batch, P);
   if (n_train != p->hdr[H_NPARAMS_TRAIN]) return fail(HPE_EINVAL, "hpe_fit_steps: n_train mismatch");
+  // every step's optimizer launch writes stats row s: [sse, sae, reg_0 .. reg_{grid-1}]
+  if ((int64_t)stats_stride < 2 + (int64_t)hpe_optim_grid(n_train))
+    return fail(HPE_EINVAL, "hpe_fit_steps: stats_stride %d < 2 + hpe_optim_grid(n_train) = %d", stats_stride,
+                2 + hpe_optim_grid(n_train));
   const int64_t steps = (n + batch - 1) / batch;
   for (int64_t s = 0; s < steps; ++s) {
     const int64_t b0 = s * batch, nb = (n - b0) < batch ? (n - b0) : batch;

@@ -227,8 +227,8 @@ extern "C" int hpe_attn_tail(const float* xg, int32_t ld_xg, const float* o, int
   hipStream_t s = (hipStream_t)stream;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return hpe_fail(HPE_ERUNTIME, "hpe_attn_tail: LDS attribute");
-  hpe_tev_begin(s);
+  const int tv = hpe_tev_begin(s);
   hipLaunchKernelGGL(k, dim3(grid), dim3(TL_NW * 64), lds, s, a);
-  hpe_tev_end(s);
+  hpe_tev_end(s, tv);
   return hipGetLastError() == hipSuccess ? 0 : hpe_fail(HPE_ERUNTIME, "hpe_attn_tail: launch failed");
 }

@@ -367,14 +367,6 @@ def compile_graph(model_config, weights, mode='fwd', P=1, T=None, NW=None, wg_pe
             ch = _try_chain(b, x_t, y_t, n_train, l2c)
             if ch is not None:
                 return ch
-        # the wide two-layer kernels (one workgroup per launch / epoch) are opt-in: measured on
-        # MI355X they lose to the mlp2 / fit kernels for train_88.py's 88-64-3 (fused epoch b128
-        # 32.6 vs 18.3 us per step, per-step b512 68.8 vs 38.4), which spread the hidden units
-        # over many workgroups; create_model_complex (16-wide blocks) keeps the residual kernels
-        if mode == 'train' and P == 1 and os.environ.get('HPE_WIDE', '0') == '1':
-            wide = _try_wide(b, x_t, y_t, n_train, l2c)
-            if wide is not None:
-                return wide
         mlp2 = _try_mlp2(b, x_t, y_t, modes[mode], n_train, l2c, P)
         if mlp2 is not None:
             return mlp2
@@ -1130,44 +1122,6 @@ def _try_res(b, x_t, y_t, n_train, l2c):
     return _fused_program(b, op + table, 3, 512, 8, MODE_TRAIN, n_train, l2c, d0.K,
                           {'kind': 'res', 'blocks': nb, 'bottleneck': bt.N if bt is not None else 0,
                            'layers': len(dense)})
-
-
-def _res_table(dense):
-    table = []
-    for x in dense:
-        ent = [0] * RL_WORDS
-        ent[0], ent[1], ent[2] = x.w[1], -1 if x.bias is None else x.bias[1], x.act
-        ent[3], ent[4], ent[5] = -1, 0, _f2i(1.0)
-        if x.drop_id >= 0:
-            ent[3], ent[4] = x.drop_id, _u2i(dropout_threshold(x.rate))
-            ent[5] = _f2i(np.float32(1.0) - np.float32(x.rate))
-        ent[6], ent[7] = x.K, x.N
-        table += ent
-    return table
-
-
-def _try_wide(b, x_t, y_t, n_train, l2c):
-    """The 2-layer create_model family with a narrow hidden layer (train_88.py:66-140 create_model,
-    88 -> 64 softsign -> 3: configs[2]) trained on 1x1 maps: x -> dense F (16 <= F <= 64, a multiple of
-    16) -> dense 3, as a KIND_RES program with no residual blocks (csrc/hpe_res.hip wide kernels:
-    one workgroup per <= 512-row launch, and the whole-epoch kernel)."""
-    f = b.fops
-    if len(f) != 2 or any(x.kind != 'dense' or x.transposed or x.w[0] != 'p' or x.act in NEEDS_Z for x in f):
-        return None
-    d0, d1 = f
-    if d0.ins[0] is not x_t or d1.ins[0] is not d0.out or d1.out is not y_t or d1.N != 3:
-        return None
-    if d0.K not in RES_CIN or d0.N % 16 or not 16 <= d0.N <= 64 or len(d0.out.consumers) != 1:
-        return None
-    if any(x.bias is not None and x.bias[0] != 'p' for x in f):
-        return None
-    op = [0] * O_WORDS
-    op[O_TYPE] = OP_RES
-    op[O_K], op[O_N], op[O_AUX3], op[O_FLAGS], op[O_MODE] = d0.K, d0.N, 0, 0, 0
-    op[O_AUX0] = H_WORDS + O_WORDS
-    op[O_AUX1] = 2
-    return _fused_program(b, op + _res_table(f), 3, 512, 8, MODE_TRAIN, n_train, l2c, d0.K,
-                          {'kind': 'res', 'blocks': 0, 'F': d0.N, 'layers': 2})
 
 
 def _fused_program(b, op, kind, T, nw, mode, n_train, l2c, cin, info):

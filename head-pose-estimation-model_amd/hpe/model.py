@@ -263,7 +263,7 @@ class Model:
         self._last_fit_fused = fused
         # one bound on the resident rows per call: below the fp16 split's data range (64) the
         # per-step launches skip their exact-fp32 twin (csrc/hpe_mlp2.hip launch_pair)
-        x_bound = 0.0 if fused else float(xd.abs().max().item()) if xd.numel() else 0.0
+        x_bound = 0.0 if fused or not xd.numel() else max(-float(xd.amin().item()), float(xd.amax().item()))
         if not np.isfinite(x_bound):
             x_bound = 0.0
         if fused:  # [sse, sae, per-wave regularisation shares of the 4 G waves]

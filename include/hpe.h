@@ -118,7 +118,9 @@ int hpe_reduce_optim_step(const hpe_program *prog, int64_t n_rows, const void *w
  * s = 0 .. ceil(n / batch) - 1 with rows perm[s*batch .. min(n, (s+1)*batch)): hpe_train_step_bounded
  * (dropout seed seed_base + iter0 + 1 + s, inv_count = (float)(1.0 / (rows * P * 3)), x_bound), then
  * hpe_reduce_optim_step when hpe_launch_grid <= 16, else hpe_reduce + hpe_optim_step, with iteration
- * iter0 + 1 + s and stats + s * stats_stride — the launches fit issues from Python, bit-identical. */
+ * iter0 + 1 + s and stats + s * stats_stride — the launches fit issues from Python, bit-identical.
+ * Each stats row receives hpe_optim_step's [sse, sae, reg_0 .. reg_{grid-1}]: stats_stride must be
+ * >= 2 + hpe_optim_grid(n_train) (HPE_EINVAL otherwise), stats holds ceil(n / batch) rows. */
 int hpe_fit_steps(const hpe_program *prog, float *params, float *params_t, float *m, float *v,
                   const float *l2, const int32_t *tpos, int64_t n_train, const float *x,
                   const float *y_true, const int32_t *perm, int64_t n, int32_t batch, int32_t P,
@@ -218,7 +220,7 @@ int hpe_kernel_times(float *ms, int32_t max);
 /* Diagnostics (race screens; synchronises the device, so not for the hot path): out[0] = the
  * program's last launch epoch, out[1 .. 16] its guard ring (word e % 16 holds e when launch e's
  * fp16-split kernel flagged a non-finite value and its exact-fp32 twin recomputed the step),
- * out[17 .. 32] which check fired per ring slot (mlp2v_kernel: 1 forward sums, 2 dW1 flush). */
+ * out[17 .. 32] reserved per ring slot for which check fired (no current kernel writes them: 0). */
 int hpe_guard_peek(const hpe_program *prog, int32_t *out);
 
 /* Precision of the regressor GEMMs (process-wide; returns the previous setting).  Default 0: the

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-2 check on the GPU box (run via gpurun): smoke, GPU parity suite, bench (all lines), and a
+# Round check on the GPU box (run via gpurun): smoke, GPU parity suite, bench (all lines), and a
 # rocprofv3 kernel trace of each bench line in its own process (profiles keyed per line).
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r02}
+TAG=${TAG:-r05}
 SKIP_TESTS=${SKIP_TESTS:-0}
 step() { echo "[$(date +%T)] $*"; }
 step smoke

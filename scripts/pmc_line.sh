@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r02}
+TAG=${TAG:-r05}
 LINE=${LINE:-train}
 ARGS="--only $LINE --no-cpu --steps ${STEPS:-5} --warmup ${WARMUP:-1}"
 if [ "${LIST:-0}" = 1 ]; then

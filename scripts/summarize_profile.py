@@ -1,4 +1,4 @@
-"""Turn the per-line profiles of scripts/gpu_r02.sh (kernel trace) and scripts/pmc_r02.sh (PMC passes)
+"""Turn the per-line profiles of scripts/gpu_evidence.sh (kernel trace) and scripts/pmc_line.sh (PMC passes)
 into committed evidence under profiles/.
 
 Every bench line is profiled in its OWN process (``bench.py --only <line>``), so a line's dispatches

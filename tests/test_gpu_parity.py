@@ -330,24 +330,15 @@ def test_train_step_bounded_matches_unbounded(rid, P, n):
     assert 0 < bound < 64
     g0 = eng.gradient(xt, yt, P, None, n, 1.0 / (n * P * 3), seed=3).cpu().numpy().copy()
     g1 = eng.gradient(xt, yt, P, None, n, 1.0 / (n * P * 3), seed=3, x_bound=bound).cpu().numpy().copy()
-    if P >= 32 and not np.array_equal(g0, g1):
-        # only with the opt-in mlp2v (DESIGN.md, mlp2v open issue): in a process's first few launches
-        # one row's dW2[:, 0] term can drop from one 16-lane group; bounded to 1e-6 of max |g|
-        d = np.abs(g0 - g1).max() / np.abs(g0).max()
-        print('P=%d: launches differ by %.2e of max |g| (%d entries)' % (P, d, int((g0 != g1).sum())))
-        assert d <= 1e-6, d
-        return
     np.testing.assert_array_equal(g0, g1)
 
 
 @pytest.mark.parametrize('F,act,dropout,side,n', [(360, 'tanh', 0.0, 96, 2), (360, 'tanh', 0.3, 8, 300),
                                                   (200, 'elu', 0.2, 6, 500), (256, 'relu', 0.1, 12, 120),
                                                   (137, 'softsign', 0.0, 33, 16), (360, 'tanh', 0.3, 8, 40)])
-def test_train_step_8wave_kernel(F, act, dropout, side, n):
-    """The fused split training step on the launches csrc/hpe_mlp2.hip's mlp2v_kernel would take
-    (P >= 32, 128 < F <= 384): since round 4 they run the 12-wave mlp2_kernel by default (mlp2v is
-    opt-in, HPE_MLP2_V=1: DESIGN.md, mlp2v open issue), so this holds the default path;
-    test_train_step_8wave_opt_in runs the same bar on mlp2v when it is opted in.  Checks the
+def test_train_step_12wave_kernel(F, act, dropout, side, n):
+    """The fused split training step of the 12-wave mlp2_kernel (csrc/hpe_mlp2.hip) at P >= 32,
+    128 < F <= 384 (the configs[3] shape and its neighbours).  Checks the
     gradient (incl. loss sums) against the exact-fp32 12-wave kernel and the float64 oracle,
     for the compiled-in tanh / softsign, the runtime-activation instantiation (elu, relu) and
     SpatialDropout on both layers; ragged row counts (n P not a multiple of the 32-row tile)."""
@@ -387,29 +378,30 @@ def test_train_step_8wave_kernel(F, act, dropout, side, n):
     np.testing.assert_allclose(g_split[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
 
 
-@pytest.mark.skipif(os.environ.get('HPE_MLP2_V') != '1', reason='mlp2v is opt-in (HPE_MLP2_V=1)')
-@pytest.mark.parametrize('F,act,side,n', [(360, 'tanh', 96, 2), (137, 'softsign', 33, 16), (256, 'relu', 12, 120)])
-def test_train_step_8wave_opt_in(F, act, side, n):
-    """mlp2v_kernel itself (opted in; launches with >= 2 tiles per workgroup and no dropout) on the
-    bar of test_train_step_8wave_kernel."""
-    test_train_step_8wave_kernel(F, act, 0.0, side, n)
-
-
 @pytest.mark.parametrize('rid,side,n,R', [('sqnu665j', 96, 2, 60), ('sqnu665j', 96, 24, 12),
-                                          ('stoqa9pt', 88, 8, 24)])
+                                          ('stoqa9pt', 88, 8, 24),
+                                          # one tile per workgroup (8 tiles on 8 workgroups / 40 tiles)
+                                          ('sqnu665j', 8, 4, 40), ('sqnu665j', 8, 40, 40),
+                                          (('tanh', 0.3), 8, 4, 40), (('tanh', 0.3), 8, 40, 40)])
 def test_train_step_repeatable(rid, side, n, R):
     """Race screen (scripts/diag_repeat.py as a test): the fused training step launched R times on
-    identical inputs must give bit-identical gradients.  sqnu665j at 96x96 runs the split 12-wave kernel (n = 2:
-    two or three tiles per workgroup, the first tile's X(t+1) staged right before forward(0); n =
-    24: the steady-state X(t+2) staging), stoqa9pt at 88x88 the 4-wave mlp2_kernel.  Round 3 saw rare
-    runs (2 in ~3,700 launches) where one row's yaw head partial differed — traced to a wave's LDS-DMA
-    still in flight across that wave's head-partial LDS writes; with the DMA landed first
-    (hpe_mlp2.hip, vmcnt(0) before the partial writes) 0 of 9,960 launches differed."""
+    identical inputs must give bit-identical gradients.  sqnu665j at 96x96 runs the split 12-wave
+    kernel (n = 2: two or three tiles per workgroup, the first tile's X(t+1) staged right before
+    forward(0); n = 24: the steady-state staging), stoqa9pt at 88x88 the 4-wave mlp2_kernel.  The
+    8x8 cases launch one 32-row tile per workgroup (the launch shape where round 4's 8-wave kernel
+    dropped dW2 row terms), without and with SpatialDropout on both layers (create_model(360, tanh,
+    0.3)), including a process's first launches."""
     from hpe.engine import Engine
-    mc, w = fixture(rid)
-    c = input_channels(mc)
-    eng = Engine(mc, w)
+    if isinstance(rid, tuple):
+        hpe.set_seed(360)
+        m = _create_model(360, rid[0], rid[1], 0.1)
+        eng, c = m._eng(), 96
+    else:
+        mc, w = fixture(rid)
+        c = input_channels(mc)
+        eng = Engine(mc, w)
     P = side * side
+    assert eng.program('train', P).prog.kind == 'mlp2'
     x = features(n, c, seed=21, h=side, w=side)
     y = labels(n, seed=22)
     xt = torch.from_numpy(x.reshape(n * P, c)).cuda()
@@ -444,7 +436,7 @@ def test_training_trajectory_wide_dropout(F, act, dropout, P):
     """the 12-wave split kernel (129 <= F <= 384) with dropout on both layers (the
     sweep.yaml grid: filters 256 / 360, dropout > 0), for the compiled-in tanh and the runtime
     activation instantiation (ACT1 = -1), against the oracle's fit with the same dropout masks;
-    at P >= 32 fit's gathered batches run the split 12-wave kernel (mlp2v_kernel when opted in)."""
+    at P >= 32 fit's gathered batches run the split 12-wave kernel."""
     hpe.set_seed(11)
     m = _create_model(F, act, dropout, 0.1)
     w0 = m.weights_dict()

@@ -45,49 +45,6 @@ def test_complex_compiles_to_res_program():
     assert eng.program('train', 1).prog.info['blocks'] == 3
 
 
-def _model88(F=64, dr=1e-4, opt=None, seed=88):
-    """train_88.py:66-140 create_model (88 -> F softsign -> SpatialDropout -> 3 -> SpatialDropout,
-    L2 1e-6 on the kernels), compiled as train_88.py:323-328."""
-    keras.backend.clear_session()
-    hpe.set_seed(seed)
-    reg = keras.regularizers.l2(1e-6)
-    inp = keras.Input(shape=(None, None, 88))
-    h = keras.layers.Conv2D(F, 1, activation='softsign', kernel_regularizer=reg)(inp)
-    h = keras.layers.SpatialDropout2D(dr)(h)
-    o = keras.layers.Conv2D(3, 1, kernel_regularizer=reg)(h)
-    o = keras.layers.SpatialDropout2D(dr)(o)
-    m = keras.Model(inp, o)
-    m.compile(optimizer=opt or keras.optimizers.Adam(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
-    return m
-
-
-@pytest.mark.parametrize('F,n,dr,gather', [(64, 512, 1e-4, False), (64, 203, 0.3, True), (32, 128, 0.2, False)])
-def test_wide_gradient_vs_float64_oracle(F, n, dr, gather, monkeypatch):
-    """create_model with a narrow hidden layer at P = 1 (the wide two-layer kernel of
-    csrc/hpe_res.hip, opt-in: HPE_WIDE=1): one training launch against the float64 oracle's
-    autograd gradient, dropout on both layers; P > 1 launches keep the mlp2 kernel."""
-    monkeypatch.setenv('HPE_WIDE', '1')
-    m = _model88(F, dr)
-    eng = m._eng()
-    prog = eng.program('train', 1).prog
-    assert prog.kind == 'res' and prog.info['blocks'] == 0
-    assert eng.program('train', 16).prog.kind == 'mlp2'
-    x = features(n, 88, seed=13)
-    y = labels(n, seed=14)
-    xt = torch.from_numpy(x.reshape(n, 88)).cuda()
-    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
-    idx = None
-    if gather:
-        perm = np.random.default_rng(9).permutation(n).astype(np.int32)
-        idx = torch.from_numpy(perm).cuda()
-        x, y = x[perm], y[perm]
-    g = eng.gradient(xt, yt, 1, idx, n, 1.0 / (n * 3), seed=17).cpu().numpy().astype(np.float64)
-    g64 = _grad64(m.model_config, m.weights_dict(), x, y, eng.layout, 17)
-    err = np.abs(g[:eng.n_train] - g64).max() / np.abs(g64).max()
-    print('wide F=%d n=%d: max |g - g64| / max |g64| = %.2e' % (F, n, err))
-    assert err <= 1e-5, err
-
-
 @pytest.mark.parametrize('n,side,dr,gather', [(128, 1, 1e-4, False), (203, 1, 0.3, False), (20, 3, 0.2, False),
                                               (77, 1, 0.1, True)])
 def test_res_gradient_vs_float64_oracle(n, side, dr, gather):
@@ -138,14 +95,12 @@ def test_res_gradient_repeatable():
         assert np.array_equal(g, ref)
 
 
-@pytest.mark.parametrize('net,opt,bs', [('complex', 'sgd', 128), ('complex', 'adam', 128), ('complex', 'adamax', 96),
-                                        ('complex', 'adam', 300), ('m88', 'adam', 512), ('m88', 'sgd', 128)])
-def test_res_fused_epoch_matches_per_step_bit_for_bit(net, opt, bs, monkeypatch):
+@pytest.mark.parametrize('opt,bs', [('sgd', 128), ('adam', 128), ('adamax', 96), ('adam', 300)])
+def test_res_fused_epoch_matches_per_step_bit_for_bit(opt, bs):
     """fit's whole-epoch launch (res_fit_kernel: gradient, then the Keras legacy optimizer in LDS)
     against the per-step path (res_train_kernel on one workgroup + hpe_reduce_optim_step): the same
     gradient code, the same summation order and the same optimizer arithmetic, so after 3 epochs
     of BIWI_Train_Enlarged rows every weight is bit-identical."""
-    monkeypatch.setenv('HPE_WIDE', '1')   # the m88 cases: the (opt-in) wide kernels
     d = np.load(DATA + '/BIWI_Train_Enlarged_features_88_0.7_1.npz')
     x = d['features'].reshape(-1, 1, 1, 88).astype(np.float32)[:700]
     y = d['poses'].reshape(-1, 1, 1, 3)[:700]
@@ -158,7 +113,7 @@ def test_res_fused_epoch_matches_per_step_bit_for_bit(net, opt, bs, monkeypatch)
     try:
         for mode in ('0', '1'):
             os.environ['HPE_FIT_FUSED'] = mode
-            m = _complex(opt=mk(), seed=5) if net == 'complex' else _model88(opt=mk(), seed=5)
+            m = _complex(opt=mk(), seed=5)
             h = m.fit(x, y, batch_size=bs, epochs=3, shuffle=True, verbose=0)
             assert m._last_fit_fused == (mode == '1')
             out[mode] = m.weights_dict()
