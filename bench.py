@@ -533,9 +533,10 @@ BLAZE_ID = 'reg1-stoqa9pt-reg2-hrchr82r-selected'
 
 def bench_blazeface(dev, iters, no_cpu):
     """Config 5: the unified BlazeFace + stoqa9pt + hrchr82r graph (reference weights), batch 1024
-    frames of 128x128x3 uniform(-1, 1), fp32.  Roofline: the fused ops are each HBM-bound by
-    design (depthwise 1.9 FLOP/B), so achieved = the plan's algorithmic bytes (every op's input +
-    output map, hpe.blazeface.work_per_image) / the measured time of the whole forward."""
+    frames of 128x128x3 uniform(-1, 1), fp32.  Roofline: achieved = the frame's compulsory HBM
+    bytes (hpe.blazeface.compulsory_bytes_per_image: input, detector outputs, taps, pose maps) /
+    the measured time of the whole forward; plan_bytes (every launch's input + output maps,
+    hpe.blazeface.work_per_image) and mfma_frac alongside."""
     from hpe import blazeface as BF
     gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
     with open(os.path.join(gdir, BLAZE_ID + '.json')) as fh:
@@ -558,18 +559,23 @@ def bench_blazeface(dev, iters, no_cpu):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / iters
     ms = e0.elapsed_time(e1) / iters
-    flop, nbytes = BF.work_per_image(bf.plan)
+    flop, plan_bytes = BF.work_per_image(bf.plan)
+    nbytes = BF.compulsory_bytes_per_image(bf.plan)
     res = {'workload': 'unified BlazeFace (16 dw/pw blocks, 4 detector heads) + stoqa9pt + hrchr82r '
                        'pose heads, reference weights, batch %d frames 128x128x3 (configs[4])' % BLAZE_B,
            'value': BLAZE_B / wall, 'unit': 'images/sec', 'ms_per_batch': wall * 1e3, 'dtype': 'fp32',
            'data': 'synthetic uniform(-1,1) frames',
+           # frac on COMPULSORY bytes (input frame + detector outputs + taps + pose maps, once each);
+           # plan_bytes = what the launches' input / output maps add up to; mfma_frac on the FLOPs
            'roofline': {'bound': 'hbm', 'achieved': nbytes * BLAZE_B / (ms * 1e-3) / 1e9,
                         'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
                         'frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
                         'traffic': _traffic('blazeface'),
                         'kernel': 'bf_stem_kernel + bf_* blocks + 2 head GEMMs + 2 regressor '
-                                  'programs (hpe_blazeface_forward + hpe_forward)',
+                                  'programs (hpe_blazeface_forward + hpe_forward), whole forward',
                         'kernel_ms': ms, 'bytes_per_launch': nbytes * BLAZE_B,
+                        'plan_bytes': plan_bytes * BLAZE_B,
+                        'plan_frac': plan_bytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
                         'flop_per_launch': flop * BLAZE_B,
                         'mfma_frac': flop * BLAZE_B / (ms * 1e-3) / PEAK_FP32}}
     if not no_cpu:

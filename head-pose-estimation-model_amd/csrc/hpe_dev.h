@@ -34,22 +34,16 @@ __device__ __forceinline__ void bar_lds() {
 
 // activation of layer 1 fixed at compile time (tanh: Model-96, softsign: Model-88); ACT1 = -1 is
 // the runtime-dispatched variant for the other activations the checkpoints use
-// short-sequence tanh / softsign for the register-resident hot loop: tanh|z| = (1-t)/(1+t),
-// t = exp(-2|z|) via v_exp_f32; absolute error <= ~2 ulp(1.0) (covered by the atol of the parity
-// tests), derivative 1 - a^2 as in Keras' TanhGrad
-__device__ __forceinline__ float fast_tanh(float z) {
-  const float t = __expf(-2.f * fabsf(z));
-  return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), z);
-}
-// the same function in 5 VALU ops, 1 - 2 / (1 + e^{2z}) (e^{2z} -> inf gives 1, -> 0 gives -1;
-// absolute error <= ~2 ulp(1.0) like fast_tanh), for the 8-wave kernel's activation phase
+// tanh in 5 VALU ops for the register-resident hot loops, 1 - 2 / (1 + e^{2z}) (e^{2z} -> inf
+// gives 1, -> 0 gives -1); absolute error <= ~2 ulp(1.0) (covered by the atol of the parity tests),
+// derivative 1 - a^2 as in Keras' TanhGrad
 __device__ __forceinline__ float fast_tanh5(float z) {
   const float e = __builtin_amdgcn_exp2f(z * 2.8853900817779268f);  // 2 log2(e)
   return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);
 }
 template <int ACT1>
 __device__ __forceinline__ float act1_f(int act, float z) {
-  if (ACT1 == ACT_TANH) return fast_tanh(z);
+  if (ACT1 == ACT_TANH) return fast_tanh5(z);
   if (ACT1 == ACT_SOFTSIGN) return z * __builtin_amdgcn_rcpf(1.f + fabsf(z));
   return act_f(ACT1 >= 0 ? ACT1 : act, z);
 }

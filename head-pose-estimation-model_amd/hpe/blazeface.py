@@ -583,8 +583,8 @@ class BlazeFace:
 
 def work_per_image(plan):
     """Algorithmic work of one 128x128 frame through the plan: FLOP = 2*MAC of the
-    convs (depthwise, pointwise, stem, heads) and the regressors; bytes = each launch's compulsory
-    HBM traffic (a per-op kernel: its input map + its output map, fp32, padded channel strides as
+    convs (depthwise, pointwise, stem, heads) and the regressors; bytes = the PLAN's traffic (each
+    launch's input and output maps, not the frame's compulsory bytes: compulsory_bytes_per_image) (a per-op kernel: its input map + its output map, fp32, padded channel strides as
     stored; the stage: its input map, the taps and the head outputs) plus the regressors' tap reads
     and pose writes."""
     words = plan['words']
@@ -626,6 +626,27 @@ def work_per_image(plan):
             cin = n
         nbytes += 4 * h * w * (c + 3)
     return flop, nbytes
+
+
+def compulsory_bytes_per_image(plan):
+    """Compulsory HBM bytes of one frame through the unified graph: the fp32
+    input frame read once, and written once each: the four detector outputs, the two taps (the
+    feature maps the caller keeps, hpe.features) and the two pose maps.  Everything else a
+    forward moves (the 64x64 / 32x32 intermediate maps, the stage input, the taps' re-read by the
+    pose heads) is plan traffic that a fully fused forward would not need (work_per_image)."""
+    st = plan['structure']
+    H, W = st['input_hw']
+    n = 4 * H * W * 3
+    heads = {hd['out']: hd['shape'] for hd in st['heads']}
+    for o in plan['det_outs']:
+        n += 4 * int(np.prod(heads[o]))
+    for t in st['taps']:
+        th, tw, c = st['shapes'][t]
+        n += 4 * th * tw * c
+    for r in st['regressors']:
+        th, tw, _ = st['shapes'][r['tap']]
+        n += 4 * th * tw * 3
+    return n
 
 
 class UnifiedModel:

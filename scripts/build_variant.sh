@@ -1,19 +1,23 @@
 #!/bin/bash
-# Build varlibs/libhpe_<name>.so with both mlp2 objects (default and MLP2_BIG) compiled from
-# <mlp2 source> with extra flags (e.g. -DMLP2_STAMPS); GPU A/B runs select it via HPE_LIB.
+# Build varlibs/libhpe_<name>.so for GPU A/B runs (selected via HPE_LIB): the in-tree csrc/ with the
+# given replacement sources, compiled by csrc/Makefile itself (same flags as the in-tree library).
+# Usage: scripts/build_variant.sh <name> [<file.hip> ...] [-- <extra hipcc flags>]
+# Each <file.hip> replaces the csrc/ file of the same basename (e.g. an older hpe_mlp2.hip saved
+# as /tmp/x/hpe_mlp2.hip).  Objects whose sources are unchanged are reused from csrc/build.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CS=$ROOT/head-pose-estimation-model_amd/csrc
-NAME=$1; shift; SRC=${1:-$CS/hpe_mlp2.hip}; [ $# -gt 0 ] && shift
-mkdir -p $ROOT/varlibs $CS/build_var
+NAME=$1; shift
+FILES=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do FILES+=("$1"); shift; done
+[ "$1" = "--" ] && shift
 make -C $CS -j8 >/dev/null
-cp "$SRC" $CS/.var_$NAME.hip
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -mllvm -amdgpu-use-amdgpu-trackers=1"
-SCHED="-mllvm -amdgpu-disable-unclustered-high-rp-reschedule -mllvm -amdgpu-disable-clustered-low-occupancy-reschedule"
-/opt/rocm/bin/hipcc $F "$@" -c -o $CS/build_var/mlp2_$NAME.o $CS/.var_$NAME.hip &
-/opt/rocm/bin/hipcc $F $SCHED -DMLP2_BIG "$@" -c -o $CS/build_var/mlp2big_$NAME.o $CS/.var_$NAME.hip &
-wait
-rm -f $CS/.var_$NAME.hip
-objs=$(ls $CS/build/*.o | grep -v "hpe_mlp2.o\|hpe_mlp2_big.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/varlibs/libhpe_$NAME.so $objs $CS/build_var/mlp2_$NAME.o $CS/build_var/mlp2big_$NAME.o
+VD=$ROOT/head-pose-estimation-model_amd/var_$NAME   # sibling of csrc/: ../../include resolves
+rm -rf $VD; mkdir -p $VD/build $ROOT/varlibs
+cp -p $CS/*.hip $CS/*.h $CS/Makefile $VD/
+cp -p $CS/build/*.o $VD/build/
+touch $VD/build/*.o
+for f in "${FILES[@]}"; do cp "$f" $VD/$(basename "$f"); touch $VD/$(basename "$f"); done
+make -C $VD -j8 OUT=$ROOT/varlibs/libhpe_$NAME.so EXTRA="$*" >/dev/null 2>$VD/build.err || { tail -20 $VD/build.err; exit 1; }
+rm -rf $VD
 echo built varlibs/libhpe_$NAME.so

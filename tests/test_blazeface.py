@@ -44,6 +44,19 @@ def test_structure_recognised():
     assert [h["shape"] for h in st["heads"]] == [(512, 1), (384, 1), (512, 16), (384, 16)]
 
 
+def test_compulsory_bytes_per_frame():
+    """bench.py's BlazeFace roofline counts each frame's compulsory HBM bytes:
+    the 128x128x3 input, the 896-anchor detector outputs (1 score + 16 box values each), the two
+    taps (16x16x88, 8x8x96) and the two 3-channel pose maps, fp32, once each."""
+    mc, w = fixture(RID)
+    plan = B.build_plan(mc, w)
+    anchors = 16 * 16 * 2 + 8 * 8 * 6
+    want = 4 * (128 * 128 * 3 + anchors * (1 + 16) + 16 * 16 * 88 + 8 * 8 * 96 + 16 * 16 * 3 + 8 * 8 * 3)
+    assert B.compulsory_bytes_per_image(plan) == want == 376064
+    # the plan's own traffic (every launch's input and output maps) is an order of magnitude more
+    assert B.work_per_image(plan)[1] > 10 * want
+
+
 @pytest.mark.parametrize('rid', UNIFIED)
 def test_plan_words_emulated_match_oracle(rid):
     mc, w = fixture(rid)
