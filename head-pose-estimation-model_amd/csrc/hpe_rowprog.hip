@@ -1489,3 +1489,51 @@ extern "C" int hpe_fit_steps(const hpe_program* p, float* params, float* params_
   }
   return HPE_OK;
 }
+
+// ---- hpe_fit_steps_dp: the same step loop for one rank of a data-parallel fit ------------------
+// Per step, the launches fit's data-parallel Python loop issues (hpe/model.py): this rank's
+// contiguous share [r0, r1) of the global batch (hpe.parallel.batch_slice), hpe_train_step_bounded
+// with img_off = r0 - b0 and the GLOBAL element count, hpe_reduce (or a zeroed gradient for an empty
+// share), the caller's all-reduce of [gradient | sse, sae, 0, 0], then hpe_optim_step — no Python
+// round trip per step besides the all-reduce hook itself.
+extern "C" int hpe_fit_steps_dp(const hpe_program* p, float* params, float* params_t, float* m, float* v,
+                                const float* l2, const int32_t* tpos, int64_t n_train, const float* x,
+                                const float* ytrue, const int32_t* perm, int64_t n, int32_t batch, int32_t P,
+                                float x_bound, int32_t kind, float lr, float b1, float b2, float eps,
+                                uint64_t seed_base, int64_t iter0, void* ws, float* grad, float* stats,
+                                int32_t stats_stride, int32_t rank, int32_t world, hpe_allreduce_fn allreduce,
+                                void* user, void* stream) {
+  if (!p || !params || !x || !ytrue || !perm || !ws || !grad || !l2 || !tpos || !stats || !allreduce)
+    return fail(HPE_EINVAL, "hpe_fit_steps_dp: null argument");
+  if (n <= 0 || batch <= 0 || P <= 0 || iter0 < 0 || world < 1 || rank < 0 || rank >= world)
+    return fail(HPE_EINVAL, "hpe_fit_steps_dp: bad shape n=%lld batch=%d P=%d rank=%d world=%d", (long long)n, batch,
+                P, rank, world);
+  if (n_train != p->hdr[H_NPARAMS_TRAIN]) return fail(HPE_EINVAL, "hpe_fit_steps_dp: n_train mismatch");
+  if ((int64_t)stats_stride < 2 + (int64_t)hpe_optim_grid(n_train))
+    return fail(HPE_EINVAL, "hpe_fit_steps_dp: stats_stride %d < 2 + hpe_optim_grid(n_train) = %d", stats_stride,
+                2 + hpe_optim_grid(n_train));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t steps = (n + batch - 1) / batch;
+  for (int64_t st = 0; st < steps; ++st) {
+    const int64_t b0 = st * batch, nb = (n - b0) < batch ? (n - b0) : batch;
+    const int64_t r0 = b0 + (nb * rank) / world, r1 = b0 + (nb * (rank + 1)) / world;
+    const int64_t it = iter0 + 1 + st;
+    const float inv = (float)(1.0 / (double)(nb * P * 3));
+    int rc;
+    if (r1 > r0) {
+      rc = hpe_train_step_bounded(p, params, params_t, x, ytrue, r1 - r0, P, perm + r0, r0 - b0, inv,
+                                  seed_base + (uint64_t)it, x_bound, ws, stream);
+      if (!rc) rc = hpe_reduce(p, (r1 - r0) * P, ws, grad, stream);
+    } else {
+      rc = hipMemsetAsync(grad, 0, (n_train + 4) * sizeof(float), s) == hipSuccess
+               ? HPE_OK : fail(HPE_ERUNTIME, "hpe_fit_steps_dp: memset");
+    }
+    if (rc) return rc;
+    if (allreduce(grad, n_train + 4, stream, user) != 0)
+      return fail(HPE_ERUNTIME, "hpe_fit_steps_dp: all-reduce hook failed at step %lld", (long long)st);
+    rc = hpe_optim_step(kind, lr, b1, b2, eps, it, 1.f, params, params_t, m, v, grad, l2, tpos, n_train,
+                        stats + st * stats_stride, stream);
+    if (rc) return rc;
+  }
+  return HPE_OK;
+}

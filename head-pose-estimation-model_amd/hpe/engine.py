@@ -218,10 +218,16 @@ class Engine:
     def optim_grid(self):
         return _lib.load().hpe_optim_grid(self.n_train)
 
-    def fit_steps(self, opt, x, y, perm, batch, stats, seed_base, x_bound=0.0, P=1):
-        """One epoch of fit's per-step path (single rank) as ONE C call: hpe_fit_steps issues, per
-        step, the launches gradient(defer_reduce=True) + optimizer_step issue from Python, with the
-        same arguments (bit-identical results) and no Python round trip between steps."""
+    # the all-reduce hook hpe_fit_steps_dp calls once per step (int (*)(float*, int64, void*, void*))
+    ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p)
+
+    def fit_steps(self, opt, x, y, perm, batch, stats, seed_base, x_bound=0.0, P=1, dist=None):
+        """One epoch of fit's per-step path as ONE C call: hpe_fit_steps issues, per step, the
+        launches gradient(defer_reduce=True) + optimizer_step issue from Python, with the same
+        arguments (bit-identical results) and no Python round trip between steps.  dist = (module,
+        group) of a data-parallel fit: hpe_fit_steps_dp runs this rank's share of every batch and
+        calls back once per step for the all-reduce of [gradient | loss sums] (torch.distributed:
+        RCCL on GPU ranks), the launches of the Python DP loop in the same order."""
         if P > 1 and self.spatial() is not None:
             raise ValueError('fit of attention heads runs on 1x1 maps (train_88.py:270-305)')
         kind = OPT_KIND[opt.kind]
@@ -233,6 +239,32 @@ class Engine:
         n = int(perm.numel())
         steps = (n + batch - 1) // batch
         ws = c.workspace(min(batch, n) * P, self.device)
+        if dist is not None and dist[0].get_world_size(dist[1]) > 1:
+            mod, grp = dist
+            errors = []
+
+            def allreduce(_buf, _n, _stream, _user):
+                try:
+                    mod.all_reduce(self.grad, group=grp)
+                    return 0
+                except Exception as e:   # surfaces as HPE_ERUNTIME from the C loop, re-raised below
+                    errors.append(e)
+                    return 1
+            hook = self.ALLREDUCE_FN(allreduce)
+            rc = lib.hpe_fit_steps_dp(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
+                                      _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),
+                                      n, int(batch), int(P), float(x_bound), kind, float(opt.learning_rate),
+                                      float(opt.beta_1), float(opt.beta_2), float(opt.epsilon),
+                                      int(seed_base) & 0xFFFFFFFFFFFFFFFF, int(self.iterations), _ptr(ws),
+                                      _ptr(self.grad), _ptr(stats), int(stats.shape[1]),
+                                      mod.get_rank(grp), mod.get_world_size(grp),
+                                      ctypes.cast(hook, ctypes.c_void_p), None, _stream())
+            if errors:
+                raise errors[0]
+            _lib.check(rc, 'hpe_fit_steps_dp')
+            self._pending = None
+            self.iterations += steps
+            return
         _lib.check(lib.hpe_fit_steps(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
                                      _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),
                                      n, int(batch), int(P), float(x_bound), kind, float(opt.learning_rate),

@@ -280,12 +280,13 @@ class Model:
                     # the epoch launch timed out and was rolled back: this and later epochs per step
                     fused = self._last_fit_fused = False
                     stats = torch.zeros((steps, 2 + og), dtype=torch.float32, device=eng.device)
-            # single rank, per-step path: the whole step loop in one C call (hpe_fit_steps: the same
-            # launches as the loop below, without a Python round trip per step); HPE_FIT_STEPS=0 keeps
-            # the Python loop
-            c_steps = not fused and world == 1 and os.environ.get('HPE_FIT_STEPS', '1') != '0'
+            # per-step path: the whole step loop in one C call (hpe_fit_steps; under data parallelism
+            # hpe_fit_steps_dp with a per-step all-reduce hook: the same launches as the loop below,
+            # without a Python round trip per step); HPE_FIT_STEPS=0 keeps the Python loop
+            c_steps = not fused and os.environ.get('HPE_FIT_STEPS', '1') != '0'
             if c_steps:
-                eng.fit_steps(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0), x_bound, P)
+                eng.fit_steps(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0), x_bound, P,
+                              dist=self._dist if world > 1 else None)
             for s in range(0 if fused or c_steps else steps):
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0

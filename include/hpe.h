@@ -128,6 +128,25 @@ int hpe_fit_steps(const hpe_program *prog, float *params, float *params_t, float
                   uint64_t seed_base, int64_t iter0, void *workspace, float *grad, float *stats,
                   int32_t stats_stride, void *stream);
 
+/* One epoch of a DATA-PARALLEL rank's fit with the step loop in C (replaces the Python step loop of
+ * hpe/model.py's distributed fit; the reference's loop: train_96.py:175-183).  Per step s over rows
+ * perm[b0 .. b0 + nb) of the global batch (b0 = s * batch): this rank's share [r0, r1) with
+ * r0 = b0 + nb * rank / world, r1 = b0 + nb * (rank + 1) / world; hpe_train_step_bounded on it
+ * (img_off = r0 - b0, inv_count = (float)(1.0 / (nb * P * 3)): the GLOBAL count) + hpe_reduce into
+ * grad (n_train + 4 floats; zeroed when the share is empty), then allreduce(grad, n_train + 4,
+ * stream, user) — the caller's sum over ranks, e.g. an RCCL all-reduce on that stream; non-zero
+ * aborts with HPE_ERUNTIME — then hpe_optim_step with iteration iter0 + 1 + s into
+ * stats + s * stats_stride (stats_stride >= 2 + hpe_optim_grid(n_train)).  Bit-identical to the
+ * per-step launches issued one by one. */
+typedef int (*hpe_allreduce_fn)(float *buf, int64_t n, void *stream, void *user);
+int hpe_fit_steps_dp(const hpe_program *prog, float *params, float *params_t, float *m, float *v,
+                     const float *l2, const int32_t *tpos, int64_t n_train, const float *x,
+                     const float *y_true, const int32_t *perm, int64_t n, int32_t batch, int32_t P,
+                     float x_bound, int32_t kind, float lr, float beta_1, float beta_2, float epsilon,
+                     uint64_t seed_base, int64_t iter0, void *workspace, float *grad, float *stats,
+                     int32_t stats_stride, int32_t rank, int32_t world, hpe_allreduce_fn allreduce,
+                     void *user, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
  * Keras fit (train_96.py:175-183, train_88.py:355-363) for the reference's own regime: 1x1 maps

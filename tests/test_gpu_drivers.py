@@ -77,13 +77,22 @@ def _dp_worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     mc, w = fx('sqnu665j')
-    H.set_seed(3)
-    m = H.model_from_config(mc, w).distribute()
-    m.compile(optimizer=kk.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
-    h = m.fit(f_(160, 96, seed=21), lb(160, seed=22), batch_size=64, epochs=2, shuffle=True, verbose=0)
+    res = {}
+    # the step loop in C (hpe_fit_steps_dp, all-reduce hook per step) and the Python loop
+    # (HPE_FIT_STEPS=0) from the same state: bit-identical weights
+    for mode in ('1', '0'):
+        os.environ['HPE_FIT_STEPS'] = mode
+        H.set_seed(3)
+        m = H.model_from_config(mc, w).distribute()
+        m.compile(optimizer=kk.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
+        h = m.fit(f_(160, 96, seed=21), lb(160, seed=22), batch_size=64, epochs=2, shuffle=True, verbose=0)
+        res[mode] = (np.asarray(h.history['loss']), m.weights_dict())
+    os.environ.pop('HPE_FIT_STEPS')
+    same = all(np.array_equal(res['1'][1][k], v) for k, v in res['0'][1].items())
+    same = same and np.array_equal(res['1'][0], res['0'][0])
     if rank == 0:
-        np.savez(out, loss=np.asarray(h.history['loss']), **{k.replace('/', '|'): v
-                                                              for k, v in m.weights_dict().items()})
+        h, wd = res['1']
+        np.savez(out, loss=h, c_equals_python=same, **{k.replace('/', '|'): v for k, v in wd.items()})
     dist.destroy_process_group()
 
 
@@ -92,6 +101,7 @@ def test_data_parallel_fit_matches_single_device(tmp_path):
     out = str(tmp_path / 'dp.npz')
     mp.spawn(_dp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     dp = np.load(out)
+    assert bool(dp['c_equals_python'])   # hpe_fit_steps_dp == the Python DP step loop, bit for bit
     mc, w = fixture('sqnu665j')
     hpe.set_seed(3)
     m = hpe.model_from_config(mc, w)
