@@ -22,6 +22,7 @@
 
 #include "../../include/hpe.h"
 #include "hpe_common.h"
+#include "hpe_dev.h"
 
 struct BfArgs {
   int f[BFO_WORDS];
@@ -942,6 +943,314 @@ static bf_fn pick_direct(int s, int dw, int nc) {
   return nullptr;
 }
 
+// ------------------------------------------------------------------------------------------------
+// front: the stem and the five blocks on the 64x64 / 32x32 maps (every layer before the stage) as
+// ONE launch, one 8-wave workgroup per frame (persistent over frames).  The per-op kernels write
+// every intermediate map to HBM and read it back (3.2 MB per frame, 58 % of the forward's time at
+// 1,024 frames); here the maps stream row by row through LDS rings — each layer's output rows
+// land in the next layer's input ring (4 rows: the 3 its 3x3 window reads + the one being
+// written) — and only the frame (196 KB) and the last block's 32x32x48 output (196 KB) touch HBM.
+//   * wave roles (fixed): w0/w1 the stem's two 32-position chunks of a 64-wide row, w2/w3 block 1,
+//     w4/w5 block 2, w6 block 3 (odd phases, s2 32-wide) and block 4 (even), w7 block 5 (odd, its
+//     rows to HBM) and the frame's input rows (LDS-DMA one phase ahead into an 8-row ring).  The
+//     pointwise weights of a wave's layers live in its registers (fp16 hi/lo pairs), the depthwise
+//     tables in LDS.
+//   * phase p (one workgroup barrier each, 76 per frame): stem row p, block-1 row p - 2, block-2
+//     row p - 4, block-3 row (p - 7) / 2, block-4 row (p - 10) / 2, block-5 row (p - 13) / 2 —
+//     every row a layer reads was written in an earlier phase, and the ring slot a layer writes
+//     (row mod 4) is one no layer reads in that phase.  The bottom padding row of each map is
+//     written as zeros by its producer, the top one and the column halos are the per-frame zeroing.
+//   * the same arithmetic as bf_stem_kernel / bf_rows_kernel (stem: fp16-split MFMA over the same K
+//     order and scales; blocks: depthwise bias + 9 taps in order, mfma_split per 8 channels in the
+//     same order, bias + residual + ReLU): the output is bit-identical to the per-op launches.
+// The geometry is the BlazeFace backbone's (host-checked against the plan records).
+// ------------------------------------------------------------------------------------------------
+#define BFF_NW 8
+#define BFF_PHASES 76
+#define BFF_INS 396        // floats per input-row slot: [4 zero][128 x 3][8 zero] (16-B aligned rows)
+template <int K> struct BffL;  // block K (1..5): input map geometry of its LDS ring
+//                                S  CINP COUTP  CS  COLS PADT PADL  WO  HO  ring offset (floats)
+template <> struct BffL<1> { static constexpr int S = 1, CINP = 24, COUTP = 24, CS = 28, COLS = 66, PADT = 1, PADL = 1, WO = 64, HO = 64, RING = 0; };
+template <> struct BffL<2> { static constexpr int S = 1, CINP = 24, COUTP = 32, CS = 28, COLS = 66, PADT = 1, PADL = 1, WO = 64, HO = 64, RING = 7392; };
+template <> struct BffL<3> { static constexpr int S = 2, CINP = 32, COUTP = 32, CS = 36, COLS = 65, PADT = 0, PADL = 0, WO = 32, HO = 32, RING = 14784; };
+template <> struct BffL<4> { static constexpr int S = 1, CINP = 32, COUTP = 40, CS = 36, COLS = 34, PADT = 1, PADL = 1, WO = 32, HO = 32, RING = 24144; };
+template <> struct BffL<5> { static constexpr int S = 1, CINP = 40, COUTP = 48, CS = 44, COLS = 34, PADT = 1, PADL = 1, WO = 32, HO = 32, RING = 29040; };
+#define BFF_RINGS 35024    // floats of the five rings (4 rows each)
+#define BFF_IN BFF_RINGS   // input ring: 8 rows of BFF_INS
+#define BFF_DW (BFF_IN + 8 * BFF_INS)
+#define BFF_DWOFF(K) (BFF_DW + ((K) > 1 ? 240 : 0) + ((K) > 2 ? 240 : 0) + ((K) > 3 ? 320 : 0) + ((K) > 4 ? 320 : 0))
+#define BFF_FLOATS (BFF_DW + 1520)
+static_assert(BffL<5>::RING + 4 * BffL<5>::COLS * BffL<5>::CS == BFF_RINGS, "front rings");
+static_assert(4 * BFF_FLOATS <= 160 * 1024, "front LDS");
+
+struct BfFrontArgs {
+  int stem[BFO_WORDS];
+  int dww[6], pww[6], pwb[6];  // parameter offsets of blocks 1..5
+  const float* params;
+  const float* src;   // frames [n][128][128][3]
+  float* dst;         // block 5's output [n][32][32][48]
+  int64_t nimg;
+};
+
+// pointwise weights of block K for this lane (output channel nc * 32 + l32, channel quads
+// c0 = 4 half + 8 k): the split_w pairs bf_rows_kernel keeps in LDS
+template <int K>
+__device__ __forceinline__ void bff_wload(const BfFrontArgs& a, f32x4 (&wr)[(BffL<K>::COUTP + 31) / 32][BffL<K>::CINP / 8],
+                                          float (&bias)[(BffL<K>::COUTP + 31) / 32], int l32, int half) {
+  using L = BffL<K>;
+  constexpr int NC = (L::COUTP + 31) / 32, NKS = L::CINP / 8;
+#pragma unroll
+  for (int nc = 0; nc < NC; ++nc) {
+    const int n = nc * 32 + l32;
+#pragma unroll
+    for (int k = 0; k < NKS; ++k)
+      wr[nc][k] = n < L::COUTP ? split_w(ld4(a.params + a.pww[K] + n * L::CINP + 4 * half + 8 * k)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bias[nc] = n < L::COUTP ? a.params[a.pwb[K] + n] : 0.f;
+  }
+}
+
+// one 32-position chunk (c) of output row oy of block K: bf_rows_kernel's compute + epilogue; the
+// output goes to block K + 1's ring (row slot oy & 3) or, for K = 5, to HBM; zero: the bottom
+// padding row (zeros)
+template <int K>
+__device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
+                                          const f32x4 (&wr)[(BffL<K>::COUTP + 31) / 32][BffL<K>::CINP / 8],
+                                          const float (&bias)[(BffL<K>::COUTP + 31) / 32], float* gout, int l32, int half) {
+  using L = BffL<K>;
+  constexpr int NC = (L::COUTP + 31) / 32, NKS = L::CINP / 8, ROW = L::COLS * L::CS;
+  f32x16 acc[NC];
+#pragma unroll
+  for (int nc = 0; nc < NC; ++nc) acc[nc] = (f32x16){};
+  const float* ring = lds + L::RING;
+  const int iy0 = oy * L::S - L::PADT;
+  if (!zero) {
+    const int colx = (32 * c + l32) * L::S * L::CS;
+    const float* r0 = ring + ((iy0 + 4) & 3) * ROW + colx;
+    const float* r1 = ring + ((iy0 + 5) & 3) * ROW + colx;
+    const float* r2 = ring + ((iy0 + 6) & 3) * ROW + colx;
+    const float* dwt = lds + BFF_DWOFF(K);
+#pragma unroll
+    for (int k = 0; k < NKS; ++k) {
+      const int c0 = 4 * half + 8 * k;
+      f32x4 av = ld4(dwt + 9 * L::CINP + c0);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const float* rp = tp < 3 ? r0 : (tp < 6 ? r1 : r2);
+        const f32x4 xv = ld4(rp + (tp % 3) * L::CS + c0);
+        const f32x4 wv = ld4(dwt + tp * L::CINP + c0);
+        av.x = fmaf(xv.x, wv.x, av.x);
+        av.y = fmaf(xv.y, wv.y, av.y);
+        av.z = fmaf(xv.z, wv.z, av.z);
+        av.w = fmaf(xv.w, wv.w, av.w);
+      }
+#pragma unroll
+      for (int nc = 0; nc < NC; ++nc) acc[nc] = mfma_split(av, wr[nc][k], acc[nc]);
+    }
+  }
+  // epilogue: lane = output channel, register g = position 32 c + 4 half + (g & 3) + 8 (g >> 2)
+#pragma unroll
+  for (int nc = 0; nc < NC; ++nc) {
+    const int n = nc * 32 + l32;
+    if (n >= L::COUTP) continue;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int x = 32 * c + 4 * half + (g & 3) + 8 * (g >> 2);
+      float v = 0.f;
+      if (!zero) {
+        v = acc[nc][g] + bias[nc];
+        if (n < L::CINP) {
+          if (L::S == 1) {
+            v += ring[(oy & 3) * ROW + (x + L::PADL) * L::CS + n];
+          } else {
+            const float* t0 = ring + ((2 * oy) & 3) * ROW + 2 * x * L::CS + n;
+            const float* t1 = ring + ((2 * oy + 1) & 3) * ROW + 2 * x * L::CS + n;
+            v += fmaxf(fmaxf(t0[0], t0[L::CS]), fmaxf(t1[0], t1[L::CS]));
+          }
+        }
+        v = v > 0.f ? v : 0.f;
+      }
+      if constexpr (K < 5) {
+        using O = BffL<K + 1>;
+        lds[O::RING + (oy & 3) * (O::COLS * O::CS) + (x + O::PADL) * O::CS + n] = v;
+      } else {
+        gout[(oy * L::WO + x) * L::COUTP + n] = v;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const float* P_ = a.params;
+  // depthwise tables of blocks 1..5 (10 x CINP each) and the input ring's zero pads, once per launch
+  {
+    const int cinp[6] = {0, 24, 24, 32, 32, 40};
+    for (int k = 1; k <= 5; ++k)
+      for (int i = threadIdx.x; i < 10 * cinp[k]; i += BFF_NW * 64) lds[BFF_DWOFF(k) + i] = P_[a.dww[k] + i];
+    for (int i = threadIdx.x; i < 2 * BFF_INS; i += BFF_NW * 64) *(f32x4*)(lds + BFF_IN + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  // per-frame prologue: zero the rings and the input slot of row -1; w7 lands input rows 0..4
+  auto frame_begin = [&](int64_t img) {
+    for (int i = threadIdx.x; i < BFF_RINGS / 4; i += BFF_NW * 64) *(f32x4*)(lds + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wave == 7) {
+      for (int i = lane; i < BFF_INS / 4; i += 64) *(f32x4*)(lds + BFF_IN + 7 * BFF_INS + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* fr = a.src + img * (128 * 128 * 3);
+      for (int r = 0; r < 5; ++r) {
+        glds16(fr + r * 384 + 4 * lane, lds_addr(lds + BFF_IN + r * BFF_INS + 4));
+        if (lane < 32) glds16(fr + r * 384 + 256 + 4 * lane, lds_addr(lds + BFF_IN + r * BFF_INS + 4 + 256));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  };
+
+  if (wave < 2) {
+    // ---- stem (bf_stem_kernel's arithmetic): 32 positions ox = 32 wave + l32 of row p ----
+    const int* f = a.stem;
+    SplitW wsp[STEM_NK];
+    float inv;
+    {
+      f32x8 v[STEM_NK];
+      float mx = 0.f;
+#pragma unroll
+      for (int s = 0; s < STEM_NK; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int q = 8 * s + j;
+          v[s][j] = q < STEM_KS ? P_[f[BFO_PWW] + l32 * 90 + half * STEM_KS + q] : 0.f;
+          mx = fmaxf(mx, fabsf(v[s][j]));
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float s1 = pow2_scale(mx, 13);
+      inv = SPLIT_INV_C / s1;
+#pragma unroll
+      for (int s = 0; s < STEM_NK; ++s) wsp[s] = split_w8(v[s] * s1);
+    }
+    const int cout = f[BFO_COUT];
+    const float bias = l32 < cout ? P_[f[BFO_PWB] + l32] : 0.f;
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        if (p <= 64) {
+          f32x16 acc = {};
+          if (p < 64) {
+            const int ox = 32 * wave + l32;
+            // input rows 2p - 1 + 3 half + k (k = ky - 3 half), slot = row mod 8; element (ky, kx, c)
+            // of the lane's 5x5 window at 1 + 6 ox + 3 kx + c within the slot (image column -1 in the pad)
+            const float* tr[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) tr[k] = lds + BFF_IN + ((2 * p - 1 + 3 * half + k + 8) & 7) * BFF_INS + 1 + 6 * ox;
+#pragma unroll
+            for (int s = 0; s < STEM_NK; ++s) {
+              f32x8 xv;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int q = 8 * s + j;
+                xv[j] = q < STEM_KS ? tr[q / 15][((q / 3) % 5) * 3 + q % 3] : 0.f;
+              }
+              acc = mfma3_dw(split_d8(xv), wsp[s], acc);
+            }
+          }
+          if (l32 < cout) {
+            using O = BffL<1>;
+            float* drow = lds + O::RING + (p & 3) * (O::COLS * O::CS) + O::PADL * O::CS + l32;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              const int x = 32 * wave + 4 * half + (g & 3) + 8 * (g >> 2);
+              float v = 0.f;
+              if (p < 64) {
+                v = fmaf(acc[g], inv, bias);
+                v = v > 0.f ? v : 0.f;
+              }
+              drow[x * O::CS] = v;
+            }
+          }
+        }
+        bar_lds();
+      }
+    }
+  } else if (wave < 4) {
+    f32x4 wr[1][3];
+    float bias[1];
+    bff_wload<1>(a, wr, bias, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        const int oy = p - 2;
+        if (oy >= 0 && oy <= 64) bff_block<1>(lds, oy, wave - 2, oy == 64, wr, bias, nullptr, l32, half);
+        bar_lds();
+      }
+    }
+  } else if (wave < 6) {
+    f32x4 wr[1][3];
+    float bias[1];
+    bff_wload<2>(a, wr, bias, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        const int oy = p - 4;
+        if (oy >= 0 && oy <= 64) bff_block<2>(lds, oy, wave - 4, oy == 64, wr, bias, nullptr, l32, half);
+        bar_lds();
+      }
+    }
+  } else if (wave == 6) {
+    f32x4 w3[1][4], w4[2][4];
+    float b3[1], b4[2];
+    bff_wload<3>(a, w3, b3, l32, half);
+    bff_wload<4>(a, w4, b4, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        if (p & 1) {
+          const int oy = (p - 7) >> 1;
+          if (p >= 7 && oy <= 32) bff_block<3>(lds, oy, 0, oy == 32, w3, b3, nullptr, l32, half);
+        } else {
+          const int oy = (p - 10) >> 1;
+          if (p >= 10 && oy <= 32) bff_block<4>(lds, oy, 0, oy == 32, w4, b4, nullptr, l32, half);
+        }
+        bar_lds();
+      }
+    }
+  } else {
+    f32x4 w5[2][5];
+    float b5[2];
+    bff_wload<5>(a, w5, b5, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      const float* fr = a.src + img * (128 * 128 * 3);
+      float* gout = a.dst + img * (32 * 32 * 48);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        // the input rows phase p + 1 adds (2p + 5, 2p + 6): zeros past the frame first, then the
+        // LDS-DMA pieces (landed before this phase's barrier)
+        if (p < 64) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int r = 2 * p + 5 + k;
+            if (r >= 128)
+              for (int i = lane; i < 96; i += 64) *(f32x4*)(lds + BFF_IN + (r & 7) * BFF_INS + 4 + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int r = 2 * p + 5 + k;
+            if (r < 128) {
+              float* d = lds + BFF_IN + (r & 7) * BFF_INS + 4;
+              glds16(fr + r * 384 + 4 * lane, lds_addr(d));
+              if (lane < 32) glds16(fr + r * 384 + 256 + 4 * lane, lds_addr(d + 256));
+            }
+          }
+        }
+        if ((p & 1) && p >= 13) bff_block<5>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar_lds();
+      }
+    }
+  }
+}
+
 struct hpe_blazeface {
   int* words;
   int n_words;
@@ -997,9 +1306,37 @@ static int check_stage(const int* f, int i, int rest) {
   return 0;
 }
 
+// the front record: its six records must be the BlazeFace backbone's stem and first five blocks as
+// bf_front_kernel hard-codes them (BffL), chained through the workspace buffers
+static int check_front(const int* f, int i, int rest) {
+  if (f[BFO_NI] != 6 || rest < 6) return hpe_fail(HPE_EINVAL, "blazeface front %d: needs the stem + 5 block records", i);
+  if (f[BFO_LDS] != 4 * BFF_FLOATS) return hpe_fail(HPE_EINVAL, "blazeface front %d: LDS %d != %d", i, f[BFO_LDS], 4 * BFF_FLOATS);
+  const int* g = f + BFO_WORDS;
+  if (g[BFO_KIND] != BF_STEM || g[BFO_H] != 128 || g[BFO_W] != 128 || g[BFO_HO] != 64 || g[BFO_WO] != 64 ||
+      g[BFO_CIN] != 3 || g[BFO_COUT] != 24 || g[BFO_STRIDE] != 2 || g[BFO_PADT] != 1 || g[BFO_PADL] != 1 ||
+      g[BFO_SRC] != BF_BUF_IMG)
+    return hpe_fail(HPE_EINVAL, "blazeface front %d: stem geometry", i);
+  struct { int s, cinp, coutp, h, ho, padt, res; } L[6] = {
+      {0}, {1, 24, 24, 64, 64, 1, BF_RES_ID}, {1, 24, 32, 64, 64, 1, BF_RES_ID}, {2, 32, 32, 64, 32, 0, BF_RES_MAXPOOL},
+      {1, 32, 40, 32, 32, 1, BF_RES_ID}, {1, 40, 48, 32, 32, 1, BF_RES_ID}};
+  int last = g[BFO_DST];
+  for (int k = 1; k <= 5; ++k) {
+    const int* b = f + (k + 1) * BFO_WORDS;
+    if ((b[BFO_KIND] != BF_ROWS && b[BFO_KIND] != BF_BLOCK) || !b[BFO_DW] || !b[BFO_RELU] || b[BFO_SPLIT] ||
+        b[BFO_STRIDE] != L[k].s || b[BFO_CINP] != L[k].cinp || b[BFO_COUTP] != L[k].coutp || b[BFO_H] != L[k].h ||
+        b[BFO_W] != L[k].h || b[BFO_HO] != L[k].ho || b[BFO_WO] != L[k].ho || b[BFO_PADT] != L[k].padt ||
+        b[BFO_PADL] != L[k].padt || b[BFO_RES] != L[k].res || b[BFO_SRC] != last || b[BFO_OSTRIDE] != L[k].coutp)
+      return hpe_fail(HPE_EINVAL, "blazeface front %d: block %d geometry", i, k);
+    last = b[BFO_DST];
+  }
+  if (last != BF_BUF_A && last != BF_BUF_B) return hpe_fail(HPE_EINVAL, "blazeface front %d: output buffer", i);
+  return 0;
+}
+
 static int check_op(const int* f, int i, int rest) {
   const int kind = f[BFO_KIND];
   if (kind == BF_STAGE) return check_stage(f, i, rest);
+  if (kind == BF_FRONT) return check_front(f, i, rest);
   if (kind != BF_STEM && kind != BF_BLOCK && kind != BF_ROWS && kind != BF_DIRECT) return hpe_fail(HPE_EINVAL, "blazeface op %d: bad kind %d", i, kind);
   if (kind == BF_DIRECT) {
     const int s = f[BFO_STRIDE], dw = f[BFO_DW], wo = f[BFO_WO], ho = f[BFO_HO];
@@ -1136,6 +1473,28 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
   const int* ops = h->words + h->words[BFH_OPS_OFF];
   for (int i = 0; i < h->nops; ++i) {
     const int* f = ops + i * BFO_WORDS;
+    if (f[BFO_KIND] == BF_FRONT) {  // the stem + five blocks as one launch, one workgroup per frame
+      BfFrontArgs fa;
+      memset(&fa, 0, sizeof fa);
+      memcpy(fa.stem, f + BFO_WORDS, sizeof fa.stem);
+      for (int k = 1; k <= 5; ++k) {
+        const int* b = f + (k + 1) * BFO_WORDS;
+        fa.dww[k] = b[BFO_DWW];
+        fa.pww[k] = b[BFO_PWW];
+        fa.pwb[k] = b[BFO_PWB];
+      }
+      fa.params = params;
+      fa.src = bufs[BF_BUF_IMG];
+      fa.dst = bufs[(f + 6 * BFO_WORDS)[BFO_DST]];
+      fa.nimg = n_images;
+      const int64_t grid = n_images < h->n_cu ? n_images : h->n_cu;
+      hipFuncSetAttribute((const void*)bf_front_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * BFF_FLOATS);
+      hipLaunchKernelGGL(bf_front_kernel, dim3((unsigned)grid), dim3(BFF_NW * 64), 4 * BFF_FLOATS, s, fa);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hpe_fail(HPE_ERUNTIME, "blazeface front %d launch: %s", i, hipGetErrorString(e));
+      i += f[BFO_NI];
+      continue;
+    }
     if (f[BFO_KIND] == BF_STAGE) {  // the next BFO_NI records as one launch, one workgroup per image
       if (n_images > 0x7fffffff) return hpe_fail(HPE_EINVAL, "blazeface_forward: batch too large");
       BfStageArgs sa;

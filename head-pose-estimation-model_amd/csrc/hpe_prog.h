@@ -92,7 +92,11 @@ enum { BFH_MAGIC = 0, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF, BFH_WORDS = 8 };
 // one workgroup per image, the map resident in LDS (bf_stage_kernel); BFO_CS = the map's channel
 // stride, BFO_ROWS / BFO_COLS = floats of the map / W^T regions, BFO_LDS = bytes.  The covered
 // records keep their per-op meaning (a reader that skips BF_STAGE computes the same outputs).
-enum { BF_STEM = 1, BF_BLOCK = 2, BF_ROWS = 3, BF_DIRECT = 4, BF_STAGE = 5 };
+// BF_FRONT: an execution record: the BFO_NI = 6 records after it (the stem and the five blocks on the
+// 64x64 / 32x32 maps of the BlazeFace backbone, BF_STEM + BF_ROWS records) run as ONE launch,
+// one workgroup per frame, the maps streamed row by row through LDS rings (bf_front_kernel); only
+// the frame and the last block's 32x32 output touch HBM.  BFO_LDS = bytes.
+enum { BF_STEM = 1, BF_BLOCK = 2, BF_ROWS = 3, BF_DIRECT = 4, BF_STAGE = 5, BF_FRONT = 6 };
 enum { BF_RES_NONE = 0, BF_RES_ID = 1, BF_RES_MAXPOOL = 2 };
 // buffers: image input, two ping-pong activations, then the six caller outputs
 enum { BF_BUF_IMG = 0, BF_BUF_A = 1, BF_BUF_B = 2, BF_BUF_OUT0 = 3, BF_NBUF = 9 };

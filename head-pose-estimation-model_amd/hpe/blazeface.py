@@ -24,7 +24,7 @@ from . import _lib
 BF_MAGIC = 0x46425048
 BFH_WORDS = 8
 (BFH_MAGIC, BFH_NOPS, BFH_ACT_FLOATS, BFH_OPS_OFF) = range(4)
-BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT, BF_STAGE = 1, 2, 3, 4, 5
+BF_STEM, BF_BLOCK, BF_ROWS, BF_DIRECT, BF_STAGE, BF_FRONT = 1, 2, 3, 4, 5, 6
 # 8x8 maps and the detector heads: persistent direct-tap kernel (HPE_BF_DIRECT=0 -> tiles); the
 # 16x16 maps measured equal either way and keep the tile kernel
 import os as _os
@@ -339,11 +339,45 @@ def _with_stage(stem_op, block_ops, head_ops):
     return [stem_op] + block_ops + head_ops
 
 
-def build_plan(model_config, weights, stage=None):
+# front (csrc bf_front_kernel): the stem and the first five blocks of the BlazeFace backbone as ONE
+# launch, the maps streamed through LDS rings; its geometry is fixed in the kernel (BffL)
+FRONT_LDS = 4 * 39712
+_FRONT_BLOCKS = [(1, 24, 24, 64, 64, 1, RES_ID), (1, 24, 32, 64, 64, 1, RES_ID), (2, 32, 32, 64, 32, 0, RES_MAXPOOL),
+                 (1, 32, 40, 32, 32, 1, RES_ID), (1, 40, 48, 32, 32, 1, RES_ID)]
+
+
+def _with_front(ops):
+    """A BF_FRONT record ahead of the stem and the first five blocks when they are the backbone
+    bf_front_kernel implements (csrc check_front); the op list unchanged otherwise."""
+    if len(ops) < 6:
+        return ops
+    g = ops[0]
+    if (g[BFO_KIND] != BF_STEM or (g[BFO_H], g[BFO_W], g[BFO_HO], g[BFO_WO], g[BFO_COUT], g[BFO_STRIDE],
+                                   g[BFO_PADT], g[BFO_PADL], g[BFO_SRC]) != (128, 128, 64, 64, 24, 2, 1, 1, BUF_IMG)):
+        return ops
+    last = g[BFO_DST]
+    for b, (s, cinp, coutp, h, ho, pad, res) in zip(ops[1:6], _FRONT_BLOCKS):
+        if (b[BFO_KIND] not in (BF_ROWS, BF_BLOCK) or not b[BFO_DW] or not b[BFO_RELU] or b[BFO_SPLIT] or
+                (b[BFO_STRIDE], b[BFO_CINP], b[BFO_COUTP], b[BFO_H], b[BFO_W], b[BFO_HO], b[BFO_WO], b[BFO_PADT],
+                 b[BFO_PADL], b[BFO_RES], b[BFO_OSTRIDE]) != (s, cinp, coutp, h, h, ho, ho, pad, pad, res, coutp)
+                or b[BFO_SRC] != last):
+            return ops
+        last = b[BFO_DST]
+    if last not in (BUF_A, BUF_B):
+        return ops
+    f = [0] * BFO_WORDS
+    f[BFO_KIND], f[BFO_NI], f[BFO_LDS] = BF_FRONT, 6, FRONT_LDS
+    return [f] + ops
+
+
+def build_plan(model_config, weights, stage=None, front=None):
     """Plan words + packed parameters.  stage: run the small-map blocks and the heads as one
-    bf_stage_kernel launch (default: env HPE_BF_STAGE, on)."""
+    bf_stage_kernel launch (default: env HPE_BF_STAGE, on); front: the stem and the 64x64 / 32x32
+    blocks as one bf_front_kernel launch (default: env HPE_BF_FRONT, on)."""
     if stage is None:
         stage = _os.environ.get('HPE_BF_STAGE', '1') != '0'
+    if front is None:
+        front = _os.environ.get('HPE_BF_FRONT', '1') != '0'
     st = parse(model_config)
     P = _Params()
     ops = []
@@ -477,6 +511,8 @@ def build_plan(model_config, weights, stage=None):
         ops.append(f)
     if stage:
         ops = _with_stage(ops[0], ops[1:1 + len(st['blocks'])], ops[1 + len(st['blocks']):])
+    if front:
+        ops = _with_front(ops)
     hdr = [0] * BFH_WORDS
     hdr[BFH_MAGIC], hdr[BFH_NOPS], hdr[BFH_ACT_FLOATS], hdr[BFH_OPS_OFF] = BF_MAGIC, len(ops), act_floats, BFH_WORDS
     words = np.asarray(hdr + [x for f in ops for x in f], dtype=np.int64)
@@ -497,12 +533,12 @@ class BlazeFace:
     """Batched forward of the unified BlazeFace + regressor graph.  ``predict(images)`` returns
     the unified model's outputs (Keras order) as numpy arrays; ``forward`` keeps them on device."""
 
-    def __init__(self, model_config, weights, device=None, stage=None):
+    def __init__(self, model_config, weights, device=None, stage=None, front=None):
         if not torch.cuda.is_available():
             raise _lib.HPEError('hpe needs a ROCm GPU (MI355X / gfx950); torch.cuda is unavailable')
         from .engine import Engine
         self.device = torch.device(device or 'cuda')
-        self.plan = build_plan(model_config, weights, stage=stage)
+        self.plan = build_plan(model_config, weights, stage=stage, front=front)
         st = self.plan['structure']
         lib = _lib.load()
         h = ctypes.c_void_p()
@@ -592,11 +628,25 @@ def work_per_image(plan):
     nbytes = 0
     off = int(words[BFH_OPS_OFF])
     staged = 0          # records left in the current stage: their maps stay in LDS
+    fronted = 0         # records left in the front: only the frame and the last output touch HBM
     for i in range(int(words[BFH_NOPS])):
         f = [int(v) for v in words[off + i * BFO_WORDS: off + (i + 1) * BFO_WORDS]]
         if f[BFO_KIND] == BF_STAGE:
             staged = f[BFO_NI]
             first = True
+            continue
+        if f[BFO_KIND] == BF_FRONT:
+            fronted = f[BFO_NI]
+            continue
+        if fronted:
+            hw_in, hw_out = f[BFO_H] * f[BFO_W], f[BFO_HO] * f[BFO_WO]
+            if f[BFO_KIND] == BF_STEM:
+                flop += 2 * hw_out * 25 * 3 * f[BFO_COUT]
+                nbytes += 4 * hw_in * 3
+            else:
+                flop += 2 * hw_out * 9 * f[BFO_CIN] + 2 * hw_out * f[BFO_CIN] * f[BFO_COUT]
+                nbytes += 4 * hw_out * f[BFO_OSTRIDE] if fronted == 1 else 0
+            fronted -= 1
             continue
         hw_in, hw_out = f[BFO_H] * f[BFO_W], f[BFO_HO] * f[BFO_WO]
         if f[BFO_KIND] == BF_STEM:

@@ -4,7 +4,7 @@ op's algorithmic bytes (its input map + its output map as stored, fp32; hpe.blaz
 its mean duration.  Writes profiles/<tag>_blaze_layers.csv.
 
 Usage: python scripts/blaze_layers.py gpurun_out/prof_blaze/run_kernel_trace.csv r05 [batch]
-(HPE_BF_STAGE=0 for a trace of the per-op plan: profiles/<tag>_blaze_layers_perop.csv)
+(HPE_BF_STAGE=0 HPE_BF_FRONT=0 for a trace of the per-op plan: profiles/<tag>_blaze_layers_perop.csv)
 """
 import csv
 import os
@@ -32,6 +32,14 @@ def launches(plan):
     i = 0
     while i < nops:
         f = recs[i]
+        if f[B.BFO_KIND] == B.BF_FRONT:
+            sub = recs[i + 1:i + 1 + f[B.BFO_NI]]
+            last = sub[-1]
+            nb = 4 * sub[0][B.BFO_H] * sub[0][B.BFO_W] * 3 + 4 * last[B.BFO_HO] * last[B.BFO_WO] * last[B.BFO_OSTRIDE]
+            out.append(('front: stem + %d blocks (128x128 -> %dx%d)' % (len(sub) - 1, last[B.BFO_HO], last[B.BFO_WO]),
+                        '%dx%d' % (last[B.BFO_HO], last[B.BFO_WO]), nb))
+            i += 1 + f[B.BFO_NI]
+            continue
         if f[B.BFO_KIND] == B.BF_STAGE:
             ni = f[B.BFO_NI]
             sub = recs[i + 1:i + 1 + ni]
@@ -59,16 +67,16 @@ def launches(plan):
     return out
 
 
-def main(trace, tag, batch=1024, stage=True):
+def main(trace, tag, batch=1024, stage=True, front=True):
     mc, w = fixture('reg1-stoqa9pt-reg2-hrchr82r-selected')
-    plan = B.build_plan(mc, w, stage=stage)
+    plan = B.build_plan(mc, w, stage=stage, front=front)
     ops = [(what, hw, nb * batch) for what, hw, nb in launches(plan)]
     nops = len(ops)
     rows = [r for r in csv.DictReader(open(trace)) if r['Kernel_Name'].startswith(('bf_', 'void bf_'))]
     durs = [[] for _ in ops]
     for i, r in enumerate(rows):
         durs[i % nops].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-9)
-    out = os.path.join(ROOT, 'profiles', '%s_blaze_layers%s.csv' % (tag, '' if stage else '_perop'))
+    out = os.path.join(ROOT, 'profiles', '%s_blaze_layers%s.csv' % (tag, '' if stage and front else '_perop'))
     tot_t = tot_b = 0.0
     with open(out, 'w') as fh:
         wr = csv.writer(fh)
@@ -88,4 +96,5 @@ def main(trace, tag, batch=1024, stage=True):
 
 if __name__ == '__main__':
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'r05',
-         int(sys.argv[3]) if len(sys.argv) > 3 else 1024, os.environ.get('HPE_BF_STAGE', '1') != '0')
+         int(sys.argv[3]) if len(sys.argv) > 3 else 1024, os.environ.get('HPE_BF_STAGE', '1') != '0',
+         os.environ.get('HPE_BF_FRONT', '1') != '0')

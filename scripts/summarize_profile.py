@@ -156,7 +156,7 @@ def summarize_line(tag, line, steps=10, warmup=2, pmc_steps=5, pmc_warmup=1):
         return res
     if line == 'blazeface':
         # one forward = every launch of the graph; forwards = dispatches of the stem (timed only)
-        nfwd = max(1, min(len(v) for k, v in groups.items() if k[0].startswith('bf_stem')))
+        nfwd = max(1, min(len(v) for k, v in groups.items() if k[0].startswith(('bf_stem', 'bf_front'))))
         tot_ns = sum(sum(v) for v in groups.values()) / nfwd
         fb = wb = 0.0
         for key, cs in ctr.items():

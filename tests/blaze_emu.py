@@ -20,7 +20,7 @@ def run(plan, images):
     bufs = {B.BUF_IMG: images.astype(np.float64)}
     for i in range(int(words[B.BFH_NOPS])):
         f = _f(words, i)
-        if f[B.BFO_KIND] == B.BF_STAGE:     # an execution record: its ops follow as ordinary records
+        if f[B.BFO_KIND] in (B.BF_STAGE, B.BF_FRONT):   # execution records: their ops follow as ordinary records
             continue
         x = bufs[f[B.BFO_SRC]]
         H, W, Ho, Wo = f[B.BFO_H], f[B.BFO_W], f[B.BFO_HO], f[B.BFO_WO]

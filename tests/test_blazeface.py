@@ -53,8 +53,10 @@ def test_compulsory_bytes_per_frame():
     anchors = 16 * 16 * 2 + 8 * 8 * 6
     want = 4 * (128 * 128 * 3 + anchors * (1 + 16) + 16 * 16 * 88 + 8 * 8 * 96 + 16 * 16 * 3 + 8 * 8 * 3)
     assert B.compulsory_bytes_per_image(plan) == want == 376064
-    # the plan's own traffic (every launch's input and output maps) is an order of magnitude more
-    assert B.work_per_image(plan)[1] > 10 * want
+    # the per-op plan's traffic (every launch's input and output maps) is an order of magnitude
+    # more; the front + stage plan keeps it within 2.5x (frame, front output, stage input / taps)
+    assert B.work_per_image(B.build_plan(mc, w, stage=False, front=False))[1] > 10 * want
+    assert B.work_per_image(plan)[1] < 2.5 * want
 
 
 @pytest.mark.parametrize('rid', UNIFIED)
@@ -121,8 +123,8 @@ def test_stage_plan_covers_small_maps_and_heads(rid):
     each tap's two detector heads right after the block producing the tap; the per-op plan
     (stage=False) holds the same records in block-then-heads order."""
     mc, w = fixture(rid)
-    recs = _records(B.build_plan(mc, w)['words'])
-    per_op = _records(B.build_plan(mc, w, stage=False)['words'])
+    recs = _records(B.build_plan(mc, w, front=False)['words'])
+    per_op = _records(B.build_plan(mc, w, stage=False, front=False)['words'])
     k = [i for i, f in enumerate(recs) if f[B.BFO_KIND] == B.BF_STAGE]
     assert len(k) == 1
     st = recs[k[0]]
@@ -140,9 +142,45 @@ def test_stage_plan_covers_small_maps_and_heads(rid):
         B.work_per_image({'words': B.build_plan(mc, w, stage=False)['words'], 'structure': B.parse(mc)})[0]
 
 
-def test_capi_validates_stage_record():
+@pytest.mark.parametrize('rid', UNIFIED)
+def test_front_plan_covers_stem_and_large_maps(rid):
+    """The plan's BF_FRONT record (bf_front_kernel) covers the stem and the five blocks on the
+    64x64 / 32x32 maps, ahead of the stage; the records after it are the per-op plan's own, and
+    the plan's HBM bytes drop to the frame, the front's 32x32x48 output and the stage's traffic."""
+    mc, w = fixture(rid)
+    recs = _records(B.build_plan(mc, w)['words'])
+    per_op = _records(B.build_plan(mc, w, front=False)['words'])
+    assert recs[0][B.BFO_KIND] == B.BF_FRONT and recs[0][B.BFO_NI] == 6
+    assert recs[0][B.BFO_LDS] == B.FRONT_LDS <= 160 * 1024
+    assert recs[1:] == per_op
+    assert recs[1][B.BFO_KIND] == B.BF_STEM and recs[6][B.BFO_HO] == 32 and recs[7][B.BFO_KIND] == B.BF_STAGE
+    plan, plan0 = B.build_plan(mc, w), B.build_plan(mc, w, front=False)
+    f1, b1 = B.work_per_image(plan)
+    f0, b0 = B.work_per_image(plan0)
+    # the 64x64x24 (x4: stem out, block 1 in / out, block 2 in), 64x64x32 (x2), 32x32x32 (x2) and
+    # 32x32x40 (x2) maps no longer touch HBM
+    assert f1 == f0 and b0 - b1 == 4 * (4096 * 24 * 4 + 4096 * 32 * 2 + 1024 * 32 * 2 + 1024 * 40 * 2)
+
+
+def test_capi_validates_front_record():
     mc, w = fixture(RID)
     words = np.ascontiguousarray(B.build_plan(mc, w)['words'], np.int32)
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.hpe_blazeface_create(words.ctypes.data_as(ctypes.c_void_p), words.size, ctypes.byref(h)) == 0
+    lib.hpe_blazeface_destroy(h)
+    base = B.BFH_WORDS
+    for off, val in ((B.BFO_NI, 5), (B.BFO_LDS, 100_000), (B.BFO_WORDS + B.BFO_COUT, 16),
+                     (3 * B.BFO_WORDS + B.BFO_COUTP, 40), (4 * B.BFO_WORDS + B.BFO_STRIDE, 1),
+                     (6 * B.BFO_WORDS + B.BFO_DST, B.BUF_OUT0)):
+        bad = words.copy()
+        bad[base + off] = val
+        assert lib.hpe_blazeface_create(bad.ctypes.data_as(ctypes.c_void_p), bad.size, ctypes.byref(h)) == 1, off
+
+
+def test_capi_validates_stage_record():
+    mc, w = fixture(RID)
+    words = np.ascontiguousarray(B.build_plan(mc, w, front=False)['words'], np.int32)
     recs = _records(words)
     k = [i for i, f in enumerate(recs) if f[B.BFO_KIND] == B.BF_STAGE][0]
     base = B.BFH_WORDS + k * B.BFO_WORDS
@@ -174,13 +212,37 @@ def test_blazeface_stage_matches_per_op_bit_for_bit(rid):
     x = torch.from_numpy(_images(37, seed=37)).cuda()
     res = {}
     for stage in (False, True):
-        bf = B.BlazeFace(mc, w, stage=stage)
+        bf = B.BlazeFace(mc, w, stage=stage, front=False)
         outs = [o.cpu().numpy() for o in bf.forward(x)]
         res[stage] = (outs, {t: v.cpu().numpy() for t, v in bf.taps.items()})
     for o, a, b in zip(B.parse(mc)['outputs'], res[False][0], res[True][0]):
         np.testing.assert_array_equal(a, b, err_msg=o)
     for t in res[False][1]:
         np.testing.assert_array_equal(res[False][1][t], res[True][1][t], err_msg=t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('rid,n', [(RID, 37), (UNIFIED[2], 5), (RID, 300)])
+def test_blazeface_front_matches_per_op_bit_for_bit(rid, n):
+    """bf_front_kernel (the stem and the five 64x64 / 32x32 blocks as one launch, maps streamed
+    through LDS rings) runs the per-op kernels' arithmetic: with and without the stage behind it,
+    every output and tap is bit-identical to the per-op plan; ragged batches, fewer frames than
+    CUs (5) and more (300: workgroups walk several frames)."""
+    import torch
+    mc, w = fixture(rid)
+    x = torch.from_numpy(_images(n, seed=n)).cuda()
+    res = {}
+    for front, stage in ((False, False), (True, False), (True, True)):
+        bf = B.BlazeFace(mc, w, stage=stage, front=front)
+        assert (B.BF_FRONT in [int(v) for v in bf.plan['words'][B.BFH_WORDS::B.BFO_WORDS]]) == front
+        outs = [o.cpu().numpy() for o in bf.forward(x)]
+        res[(front, stage)] = (outs, {t: v.cpu().numpy() for t, v in bf.taps.items()})
+    ref = res[(False, False)]
+    for key in ((True, False), (True, True)):
+        for o, a, b in zip(B.parse(mc)['outputs'], ref[0], res[key][0]):
+            np.testing.assert_array_equal(a, b, err_msg='%s %s' % (key, o))
+        for t in ref[1]:
+            np.testing.assert_array_equal(ref[1][t], res[key][1][t], err_msg='%s %s' % (key, t))
 
 
 @pytest.mark.gpu
