@@ -950,9 +950,11 @@ static bf_fn pick_direct(int s, int dw, int nc) {
 // 1,024 frames); here the maps stream row by row through LDS rings — each layer's output rows
 // land in the next layer's input ring (4 rows: the 3 its 3x3 window reads + the one being
 // written) — and only the frame (196 KB) and the last block's 32x32x48 output (196 KB) touch HBM.
-//   * wave roles (fixed): w0/w1 the stem's two 32-position chunks of a 64-wide row, w2/w3 block 1,
-//     w4/w5 block 2, w6 block 3 (odd phases, s2 32-wide) and block 4 (even), w7 block 5 (odd, its
-//     rows to HBM) and the frame's input rows (LDS-DMA one phase ahead into an 8-row ring).  The
+//   * wave roles (fixed; waves w and w + 4 share a SIMD): w0/w1 the stem's two 32-position chunks of
+//     a 64-wide row, w2/w3 block 1, w4/w5 block 2, w6 block 3 (odd phases, s2 32-wide) and the
+//     frame's input rows (LDS-DMA two phases ahead into a 10-row ring: a phase waits only for the
+//     pieces issued in the phase before it, not for its own), w7 block 4 (even) and block 5 (odd,
+//     its rows to HBM).  The
 //     pointwise weights of a wave's layers live in its registers (fp16 hi/lo pairs), the depthwise
 //     tables in LDS.
 //   * phase p (one workgroup barrier each, 76 per frame): stem row p, block-1 row p - 2, block-2
@@ -966,6 +968,11 @@ static bf_fn pick_direct(int s, int dw, int nc) {
 // The geometry is the BlazeFace backbone's (host-checked against the plan records).
 // ------------------------------------------------------------------------------------------------
 #define BFF_NW 8
+#ifdef BFF_STAMPS   // per-wave busy cycles (task time, barrier waits excluded) of workgroup 0
+#define BFF_BAR() do { bff_busy += __builtin_amdgcn_s_memtime() - bff_t0; bar_lds(); bff_t0 = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BFF_BAR() bar_lds()
+#endif
 #define BFF_PHASES 76
 #define BFF_INS 396        // floats per input-row slot: [4 zero][128 x 3][8 zero] (16-B aligned rows)
 template <int K> struct BffL;  // block K (1..5): input map geometry of its LDS ring
@@ -976,8 +983,9 @@ template <> struct BffL<3> { static constexpr int S = 2, CINP = 32, COUTP = 32, 
 template <> struct BffL<4> { static constexpr int S = 1, CINP = 32, COUTP = 40, CS = 36, COLS = 34, PADT = 1, PADL = 1, WO = 32, HO = 32, RING = 24144; };
 template <> struct BffL<5> { static constexpr int S = 1, CINP = 40, COUTP = 48, CS = 44, COLS = 34, PADT = 1, PADL = 1, WO = 32, HO = 32, RING = 29040; };
 #define BFF_RINGS 35024    // floats of the five rings (4 rows each)
-#define BFF_IN BFF_RINGS   // input ring: 8 rows of BFF_INS
-#define BFF_DW (BFF_IN + 8 * BFF_INS)
+#define BFF_NIN 10         // input ring rows: 6 read per phase + 2 landing + 2 in flight
+#define BFF_IN BFF_RINGS   // input ring: BFF_NIN rows of BFF_INS
+#define BFF_DW (BFF_IN + BFF_NIN * BFF_INS)
 #define BFF_DWOFF(K) (BFF_DW + ((K) > 1 ? 240 : 0) + ((K) > 2 ? 240 : 0) + ((K) > 3 ? 320 : 0) + ((K) > 4 ? 320 : 0))
 #define BFF_FLOATS (BFF_DW + 1520)
 static_assert(BffL<5>::RING + 4 * BffL<5>::COLS * BffL<5>::CS == BFF_RINGS, "front rings");
@@ -1013,9 +1021,20 @@ __device__ __forceinline__ void bff_wload(const BfFrontArgs& a, f32x4 (&wr)[(Bff
 // output goes to block K + 1's ring (row slot oy & 3) or, for K = 5, to HBM; zero: the bottom
 // padding row (zeros)
 template <int K>
+__device__ __forceinline__ void bff_dwload(const BfFrontArgs& a, f32x4 (&dwr)[BffL<K>::CINP / 8][10], int half) {
+#pragma unroll
+  for (int k = 0; k < BffL<K>::CINP / 8; ++k)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) dwr[k][t] = ld4(a.params + a.dww[K] + t * BffL<K>::CINP + 4 * half + 8 * k);
+}
+
+// DWR: the depthwise table of the lane's channel quads in registers (dwr, bff_dwload) instead of
+// 10 ds_read_b128 per K-step from the LDS copy (the front is LDS-bandwidth-bound)
+template <int K, bool DWR = false>
 __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
                                           const f32x4 (&wr)[(BffL<K>::COUTP + 31) / 32][BffL<K>::CINP / 8],
-                                          const float (&bias)[(BffL<K>::COUTP + 31) / 32], float* gout, int l32, int half) {
+                                          const float (&bias)[(BffL<K>::COUTP + 31) / 32], float* gout, int l32, int half,
+                                          const f32x4 (*dwr)[10] = nullptr) {
   using L = BffL<K>;
   constexpr int NC = (L::COUTP + 31) / 32, NKS = L::CINP / 8, ROW = L::COLS * L::CS;
   f32x16 acc[NC];
@@ -1032,12 +1051,12 @@ __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
 #pragma unroll
     for (int k = 0; k < NKS; ++k) {
       const int c0 = 4 * half + 8 * k;
-      f32x4 av = ld4(dwt + 9 * L::CINP + c0);
+      f32x4 av = DWR ? dwr[k][9] : ld4(dwt + 9 * L::CINP + c0);
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) {
         const float* rp = tp < 3 ? r0 : (tp < 6 ? r1 : r2);
         const f32x4 xv = ld4(rp + (tp % 3) * L::CS + c0);
-        const f32x4 wv = ld4(dwt + tp * L::CINP + c0);
+        const f32x4 wv = DWR ? dwr[k][tp] : ld4(dwt + tp * L::CINP + c0);
         av.x = fmaf(xv.x, wv.x, av.x);
         av.y = fmaf(xv.y, wv.y, av.y);
         av.z = fmaf(xv.z, wv.z, av.z);
@@ -1084,21 +1103,25 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float* P_ = a.params;
+#ifdef BFF_STAMPS
+  uint64_t bff_busy = 0, bff_t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t bff_start = bff_t0;
+#endif
   // depthwise tables of blocks 1..5 (10 x CINP each) and the input ring's zero pads, once per launch
   {
     const int cinp[6] = {0, 24, 24, 32, 32, 40};
     for (int k = 1; k <= 5; ++k)
       for (int i = threadIdx.x; i < 10 * cinp[k]; i += BFF_NW * 64) lds[BFF_DWOFF(k) + i] = P_[a.dww[k] + i];
-    for (int i = threadIdx.x; i < 2 * BFF_INS; i += BFF_NW * 64) *(f32x4*)(lds + BFF_IN + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < BFF_NIN * BFF_INS / 4; i += BFF_NW * 64) *(f32x4*)(lds + BFF_IN + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  // per-frame prologue: zero the rings and the input slot of row -1; w7 lands input rows 0..4
+  // per-frame prologue: zero the rings and the input slot of row -1; w6 lands input rows 0..6
   auto frame_begin = [&](int64_t img) {
     for (int i = threadIdx.x; i < BFF_RINGS / 4; i += BFF_NW * 64) *(f32x4*)(lds + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (wave == 7) {
-      for (int i = lane; i < BFF_INS / 4; i += 64) *(f32x4*)(lds + BFF_IN + 7 * BFF_INS + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wave == 6) {
+      for (int i = lane; i < BFF_INS / 4; i += 64) *(f32x4*)(lds + BFF_IN + (BFF_NIN - 1) * BFF_INS + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
       const float* fr = a.src + img * (128 * 128 * 3);
-      for (int r = 0; r < 5; ++r) {
+      for (int r = 0; r < 7; ++r) {
         glds16(fr + r * 384 + 4 * lane, lds_addr(lds + BFF_IN + r * BFF_INS + 4));
         if (lane < 32) glds16(fr + r * 384 + 256 + 4 * lane, lds_addr(lds + BFF_IN + r * BFF_INS + 4 + 256));
       }
@@ -1139,11 +1162,11 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
           f32x16 acc = {};
           if (p < 64) {
             const int ox = 32 * wave + l32;
-            // input rows 2p - 1 + 3 half + k (k = ky - 3 half), slot = row mod 8; element (ky, kx, c)
+            // input rows 2p - 1 + 3 half + k (k = ky - 3 half), slot = row mod BFF_NIN; element (ky, kx, c)
             // of the lane's 5x5 window at 1 + 6 ox + 3 kx + c within the slot (image column -1 in the pad)
             const float* tr[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) tr[k] = lds + BFF_IN + ((2 * p - 1 + 3 * half + k + 8) & 7) * BFF_INS + 1 + 6 * ox;
+            for (int k = 0; k < 3; ++k) tr[k] = lds + BFF_IN + ((2 * p - 1 + 3 * half + k + BFF_NIN) % BFF_NIN) * BFF_INS + 1 + 6 * ox;
 #pragma unroll
             for (int s = 0; s < STEM_NK; ++s) {
               f32x8 xv;
@@ -1170,85 +1193,99 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
             }
           }
         }
-        bar_lds();
+        BFF_BAR();
       }
     }
   } else if (wave < 4) {
-    f32x4 wr[1][3];
+    f32x4 wr[1][3], dwr[3][10];
     float bias[1];
     bff_wload<1>(a, wr, bias, l32, half);
+    bff_dwload<1>(a, dwr, half);
     for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
       frame_begin(img);
       for (int p = 0; p < BFF_PHASES; ++p) {
         const int oy = p - 2;
-        if (oy >= 0 && oy <= 64) bff_block<1>(lds, oy, wave - 2, oy == 64, wr, bias, nullptr, l32, half);
-        bar_lds();
+        if (oy >= 0 && oy <= 64) bff_block<1, true>(lds, oy, wave - 2, oy == 64, wr, bias, nullptr, l32, half, dwr);
+        BFF_BAR();
       }
     }
   } else if (wave < 6) {
-    f32x4 wr[1][3];
+    f32x4 wr[1][3], dwr[3][10];
     float bias[1];
     bff_wload<2>(a, wr, bias, l32, half);
+    bff_dwload<2>(a, dwr, half);
     for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
       frame_begin(img);
       for (int p = 0; p < BFF_PHASES; ++p) {
         const int oy = p - 4;
-        if (oy >= 0 && oy <= 64) bff_block<2>(lds, oy, wave - 4, oy == 64, wr, bias, nullptr, l32, half);
-        bar_lds();
+        if (oy >= 0 && oy <= 64) bff_block<2, true>(lds, oy, wave - 4, oy == 64, wr, bias, nullptr, l32, half, dwr);
+        BFF_BAR();
       }
     }
   } else if (wave == 6) {
-    f32x4 w3[1][4], w4[2][4];
-    float b3[1], b4[2];
+    f32x4 w3[1][4];
+    float b3[1];
     bff_wload<3>(a, w3, b3, l32, half);
-    bff_wload<4>(a, w4, b4, l32, half);
     for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
       frame_begin(img);
+      const float* fr = a.src + img * (128 * 128 * 3);
       for (int p = 0; p < BFF_PHASES; ++p) {
         if (p & 1) {
           const int oy = (p - 7) >> 1;
           if (p >= 7 && oy <= 32) bff_block<3>(lds, oy, 0, oy == 32, w3, b3, nullptr, l32, half);
+        }
+        // the input rows phase p + 2 adds (2p + 7, 2p + 8): zeros past the frame, LDS-DMA pieces
+        // otherwise; then wait for the pieces of phase p - 1 only (this phase's stay in flight)
+        int nd = 0;
+        if (p < 62) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {   // zero rows first: no LDS write behind this phase's pieces
+            const int r = 2 * p + 7 + k;
+            if (r >= 128)
+              for (int i = lane; i < 96; i += 64) *(f32x4*)(lds + BFF_IN + (r % BFF_NIN) * BFF_INS + 4 + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int r = 2 * p + 7 + k;
+            if (r < 128) {
+              float* d = lds + BFF_IN + (r % BFF_NIN) * BFF_INS + 4;
+              glds16(fr + r * 384 + 4 * lane, lds_addr(d));
+              if (lane < 32) glds16(fr + r * 384 + 256 + 4 * lane, lds_addr(d + 256));
+              nd += 2;
+            }
+          }
+        }
+        if (nd == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (nd == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        BFF_BAR();
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    f32x4 w4[2][4], w5[2][5];
+    float b4[2], b5[2];
+    bff_wload<4>(a, w4, b4, l32, half);
+    bff_wload<5>(a, w5, b5, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      float* gout = a.dst + img * (32 * 32 * 48);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        if (p & 1) {
+          if (p >= 13) bff_block<5>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
         } else {
           const int oy = (p - 10) >> 1;
           if (p >= 10 && oy <= 32) bff_block<4>(lds, oy, 0, oy == 32, w4, b4, nullptr, l32, half);
         }
-        bar_lds();
-      }
-    }
-  } else {
-    f32x4 w5[2][5];
-    float b5[2];
-    bff_wload<5>(a, w5, b5, l32, half);
-    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
-      frame_begin(img);
-      const float* fr = a.src + img * (128 * 128 * 3);
-      float* gout = a.dst + img * (32 * 32 * 48);
-      for (int p = 0; p < BFF_PHASES; ++p) {
-        // the input rows phase p + 1 adds (2p + 5, 2p + 6): zeros past the frame first, then the
-        // LDS-DMA pieces (landed before this phase's barrier)
-        if (p < 64) {
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int r = 2 * p + 5 + k;
-            if (r >= 128)
-              for (int i = lane; i < 96; i += 64) *(f32x4*)(lds + BFF_IN + (r & 7) * BFF_INS + 4 + 4 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int r = 2 * p + 5 + k;
-            if (r < 128) {
-              float* d = lds + BFF_IN + (r & 7) * BFF_INS + 4;
-              glds16(fr + r * 384 + 4 * lane, lds_addr(d));
-              if (lane < 32) glds16(fr + r * 384 + 256 + 4 * lane, lds_addr(d + 256));
-            }
-          }
-        }
-        if ((p & 1) && p >= 13) bff_block<5>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar_lds();
+        BFF_BAR();
       }
     }
   }
+#ifdef BFF_STAMPS
+  if (blockIdx.x == 0 && lane == 0)
+    printf("BFF w%d busy %llu total %llu\n", wave, (unsigned long long)bff_busy,
+           (unsigned long long)(__builtin_amdgcn_s_memtime() - bff_start));
+#endif
 }
 
 struct hpe_blazeface {

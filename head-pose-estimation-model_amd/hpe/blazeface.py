@@ -341,7 +341,7 @@ def _with_stage(stem_op, block_ops, head_ops):
 
 # front (csrc bf_front_kernel): the stem and the first five blocks of the BlazeFace backbone as ONE
 # launch, the maps streamed through LDS rings; its geometry is fixed in the kernel (BffL)
-FRONT_LDS = 4 * 39712
+FRONT_LDS = 4 * 40504
 _FRONT_BLOCKS = [(1, 24, 24, 64, 64, 1, RES_ID), (1, 24, 32, 64, 64, 1, RES_ID), (2, 32, 32, 64, 32, 0, RES_MAXPOOL),
                  (1, 32, 40, 32, 32, 1, RES_ID), (1, 40, 48, 32, 32, 1, RES_ID)]
 

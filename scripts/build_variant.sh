@@ -18,6 +18,8 @@ cp -p $CS/*.hip $CS/*.h $CS/Makefile $VD/
 cp -p $CS/build/*.o $VD/build/
 touch $VD/build/*.o
 for f in "${FILES[@]}"; do cp "$f" $VD/$(basename "$f"); touch $VD/$(basename "$f"); done
+# extra flags: every object is rebuilt with them except the (slow) residual-stack kernels
+[ $# -gt 0 ] && ls $VD/build/*.o | grep -v "hpe_res[0-9]" | xargs rm -f
 make -C $VD -j8 OUT=$ROOT/varlibs/libhpe_$NAME.so EXTRA="$*" >/dev/null 2>$VD/build.err || { tail -20 $VD/build.err; exit 1; }
 rm -rf $VD
 echo built varlibs/libhpe_$NAME.so
