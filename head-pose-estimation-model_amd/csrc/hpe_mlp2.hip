@@ -209,6 +209,9 @@ __device__ __forceinline__ void presplit_tile(const float* xs, _Float16* xf, _Fl
 template <int KH, int ACT1, bool DROP, int NWM, bool SPLIT>
 __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(NWM == MLP2_MAXW || ACT1 < 0 ? 1 : MLP2_W88, 8))) mlp2_kernel(Args args) {
   if (!SPLIT && args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
+#ifdef MLP2_STAMPS
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NKB = (2 * KH + 31) / 32;  // 32-row blocks of dW1 (input channels)
   constexpr int T = 32;
@@ -367,6 +370,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
 #ifdef MLP2_STAMPS
   uint32_t ph[9] = {};
   uint64_t tprev = __builtin_amdgcn_s_memtime();
+  const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
 #define STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[i] += (uint32_t)(t_ - tprev); tprev = t_; } while (0)
 #else
 #define STAMP(i) do {} while (0)
@@ -642,6 +646,8 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   }
 
 #ifdef MLP2_STAMPS
+  const uint64_t rt2 = __builtin_amdgcn_s_memrealtime();
+  uint64_t rtA = 0, rtB = 0;
   if (PRE && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 5))
     printf("STAMP w%d bwd+tail %u bar1 %u stage %u fwdmfma %u act+part %u bar2 %u head %u bar3 %u presplit %u\n", wave,
            ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
@@ -655,9 +661,14 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
   const int npt = prog[H_NPARAMS_TRAIN];
   float* ws = args.ws + (size_t)blockIdx.x * slab;
   const float sc = SPLIT ? args.inv_count : 1.f;  // the split path carries unnormalised gradients
+  // slab offsets in registers: read through `o` at each store, the compiler reloads them behind a
+  // vmcnt(0) per store (ws may alias the program) — 48 serial round trips, 17 us of a one-tile launch
+  const int oW = __builtin_amdgcn_readfirstlane(o[O_W]), oB = __builtin_amdgcn_readfirstlane(o[O_BIAS]);
+  const int oA0 = __builtin_amdgcn_readfirstlane(o[O_AUX0]), oA1 = __builtin_amdgcn_readfirstlane(o[O_AUX1]);
   __syncthreads();
   const float s2f = colt[n * 4 + 2];
   if (train) {
+    const float scw = SPLIT ? sc * (SPLIT_INV_C / s2f) : sc;
     float chk = 0.f;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
@@ -665,7 +676,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        if (k < Cin && nok) ws[o[O_W] + (size_t)k * F + n] = dw[kb][g] * (SPLIT ? sc * (SPLIT_INV_C / s2f) : sc);
+        if (k < Cin && nok) ws[oW + (size_t)k * F + n] = dw[kb][g] * scw;
       }
     }
     if (SPLIT) bad |= !(fabsf(chk) <= 3.0e38f);
@@ -674,18 +685,32 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
 #pragma unroll
     for (int j = 0; j < 3; ++j) t2[j] = dw2[j] + __shfl_xor(dw2[j], 32, 64);
     if (half == 0 && nok) {
-      if (o[O_BIAS] >= 0) ws[o[O_BIAS] + n] = tb * sc;
+      if (oB >= 0) ws[oB + n] = tb * sc;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) ws[o[O_AUX0] + n * 3 + j] = t2[j] * sc;
+      for (int j = 0; j < 3; ++j) ws[oA0 + n * 3 + j] = t2[j] * sc;
     }
-    // db2: per-thread accumulators of output j = tid % 3 -> fixed-order sum
-    if (threadIdx.x < 3 && o[O_AUX1] >= 0) {
-      float s = 0.f;
-      for (int i = threadIdx.x; i < NT3; i += 3) s += hacc[i * HS + 2];
-      ws[o[O_AUX1] + threadIdx.x] = s * sc;
+#ifdef MLP2_STAMPS
+    rtA = __builtin_amdgcn_s_memrealtime();
+#endif
+    // db2: output j's per-thread accumulators (threads i = j mod 3 below NT3), fixed order: lane q
+    // sums i = j + 3 q, j + 3 (q + 64), ..., then one wave sum (was one thread's serial pass over
+    // NT3 / 3 LDS reads: 10 us of a one-tile launch)
+    if (oA1 >= 0) {
+      for (int j = wave; j < 3; j += NT >> 6) {
+        float s = 0.f;
+        for (int i = j + 3 * lane; i < NT3; i += 192) s += hacc[i * HS + 2];
+        s = wave_sum(s);
+        if (lane == 0) ws[oA1 + j] = s * sc;
+      }
     }
+#ifdef MLP2_STAMPS
+    rtB = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();
   }
+#ifdef MLP2_STAMPS
+  const uint64_t rtC = __builtin_amdgcn_s_memrealtime();
+#endif
   if (SPLIT && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float a = wave_sum(hacc[threadIdx.x * HS + 0]), b = wave_sum(hacc[threadIdx.x * HS + 1]);
   if (lane == 0) { red[wave] = a; red[MLP2_MAXW + wave] = b; }
@@ -697,6 +722,14 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     ws[npt] = s0;
     ws[npt + 1] = s1;
   }
+#ifdef MLP2_STAMPS
+  if (PRE && threadIdx.x == 0) {
+    const uint64_t rt3 = __builtin_amdgcn_s_memrealtime();
+    printf("RT wg %d t0 %llu pro %llu loop %llu flush %llu wstore %llu db2 %llu sync %llu tail %llu\n", (int)blockIdx.x, (unsigned long long)rt0,
+           (unsigned long long)(rt1 - rt0), (unsigned long long)(rt2 - rt1), (unsigned long long)(rt3 - rt2),
+           (unsigned long long)(rtA - rt2), (unsigned long long)(rtB - rtA), (unsigned long long)(rtC - rtB), (unsigned long long)(rt3 - rtC));
+  }
+#endif
 }
 
 // ---- host-side dispatch ---------------------------------------------------------------------
