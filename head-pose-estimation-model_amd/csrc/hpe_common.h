@@ -78,8 +78,13 @@ struct Epi {
   float keep;
 };
 
+// program words read through the constant address space: the words never change during a launch,
+// so uniform reads become scalar loads instead of vector loads that the compiler must re-issue
+// (behind a vmcnt(0)) after every store it cannot prove disjoint from the program
+typedef const __attribute__((address_space(4))) int pword;
+
 struct Ctx {
-  const int* prog;
+  const pword* prog;
   const float* params;
   const float* params_t;
   float* lds;
@@ -95,7 +100,8 @@ __device__ __forceinline__ int slot_w(const Ctx& c, int s, int w) {
   return c.prog[c.prog[H_SLOTS_OFF] + s * S_WORDS + w];
 }
 
-__device__ __forceinline__ Epi load_epi(const int* o) {
+template <typename W>
+__device__ __forceinline__ Epi load_epi(const W* o) {
   Epi e;
   e.act = o[O_EACT];
   e.drop = o[O_EDROP];

@@ -69,7 +69,7 @@ __device__ __forceinline__ void for_rc(int T, int C, F&& f) {
 // 16-byte weight load per fragment instead of 16 scalar loads.  A non-finite accumulator (data
 // outside the split's range) sets *bad -> the exact-fp32 twin re-runs the launch.
 template <int NW>
-__device__ __forceinline__ void op_dense_split(const Ctx& c, const int* o, const float* wsplit, bool& bad) {
+__device__ __forceinline__ void op_dense_split(const Ctx& c, const pword* o, const float* wsplit, bool& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
   const int sa = o[O_A], so = o[O_OUT];
   const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) split_weights_kernel(const int* __restric
 }
 
 template <int NW>
-__device__ __forceinline__ void op_dense(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_dense(const Ctx& c, const pword* o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
   const int sa = o[O_A], so = o[O_OUT];
   const int a_off = slot_w(c, sa, S_OFF), a_cp = slot_w(c, sa, S_CP), a_st = slot_w(c, sa, S_STRIDE);
@@ -253,7 +253,7 @@ __device__ __forceinline__ void zero_pads(const Ctx& c, int slot, int C) {
 // threads, partials through LDS scratch, summed in fixed order (deterministic).
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_tdense(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_tdense(const Ctx& c, const pword* o) {
   constexpr int NT = NW * 64;
   const int sa = o[O_A], so = o[O_OUT];
   const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
@@ -293,7 +293,7 @@ __device__ __forceinline__ void op_tdense(const Ctx& c, const int* o) {
 // scale / standalone SpatialDropout) with the fused epilogue.
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_ew(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_ew(const Ctx& c, const pword* o) {
   constexpr int NT = NW * 64;
   const int flags = o[O_FLAGS];
   const int C = slot_w(c, o[O_OUT], S_C);
@@ -322,7 +322,7 @@ __device__ __forceinline__ void op_ew(const Ctx& c, const int* o) {
 // wave64 shuffle reductions).  Training keeps xhat and rstd for OP_LNB.
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_ln(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_ln(const Ctx& c, const pword* o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int C = slot_w(c, o[O_A], S_C);
   const int a_off = slot_w(c, o[O_A], S_OFF), a_st = slot_w(c, o[O_A], S_STRIDE);
@@ -384,7 +384,7 @@ __device__ __forceinline__ void op_ln(const Ctx& c, const int* o) {
 // producer's epilogue (mse: train_96.py:51; labels (B,1,1,3) broadcast over H,W)
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_loss(const Ctx& c, const int* o, const float* __restrict__ ytrue,
+__device__ __forceinline__ void op_loss(const Ctx& c, const pword* o, const float* __restrict__ ytrue,
                                         const int* __restrict__ idx, float inv_count, bool train,
                                         float& sse, float& sae) {
   constexpr int NT = NW * 64;
@@ -416,7 +416,7 @@ __device__ __forceinline__ void op_loss(const Ctx& c, const int* o, const float*
 // OP_EPIGRAD: out[r][c] <- out[r][c] * epi'(value) in place
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_epigrad(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_epigrad(const Ctx& c, const pword* o) {
   constexpr int NT = NW * 64;
   const int C = slot_w(c, o[O_OUT], S_C);
   const int v_off = slot_w(c, o[O_A], S_OFF), v_st = slot_w(c, o[O_A], S_STRIDE);
@@ -431,7 +431,7 @@ __device__ __forceinline__ void op_epigrad(const Ctx& c, const int* o) {
 }
 
 // destination write of a backward result (STORE / ACCUM / EPIGRAD through the producer of `val`)
-__device__ __forceinline__ void dst_write(const Ctx& c, const int* o, int mode, const Epi& e,
+__device__ __forceinline__ void dst_write(const Ctx& c, const pword* o, int mode, const Epi& e,
                                           int d_off, int d_st, int v_off, int v_st, int z_off,
                                           int z_st, int r, int ch, float v) {
   float* p = c.lds + d_off + r * d_st + ch;
@@ -448,7 +448,7 @@ __device__ __forceinline__ void dst_write(const Ctx& c, const int* o, int mode, 
 // optimizer) so B rows stay coalesced.  Same MFMA tiling as OP_DENSE.
 // ------------------------------------------------------------------------------------------------
 template <int NW>
-__device__ __forceinline__ void op_din(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_din(const Ctx& c, const pword* o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, l32 = lane & 31;
   const int sa = o[O_A], so = o[O_OUT];
   const int a_off = slot_w(c, sa, S_OFF), a_cp = slot_w(c, sa, S_CP), a_st = slot_w(c, sa, S_STRIDE);
@@ -503,7 +503,7 @@ __device__ __forceinline__ void op_din(const Ctx& c, const int* o) {
 
 // OP_TDIN: thin contraction (N <= 8): out[r][k] (=|+=|epigrad) sum_n a[r][n] W[k][n]
 template <int NW>
-__device__ __forceinline__ void op_tdin(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_tdin(const Ctx& c, const pword* o) {
   constexpr int NT = NW * 64;
   const int sa = o[O_A], so = o[O_OUT];
   const int a_off = slot_w(c, sa, S_OFF), a_st = slot_w(c, sa, S_STRIDE);
@@ -528,7 +528,7 @@ __device__ __forceinline__ void op_tdin(const Ctx& c, const int* o) {
 
 // OP_EWB: backward of OP_EW (its epilogue already applied by OP_EPIGRAD / fused producer)
 template <int NW>
-__device__ __forceinline__ void op_ewb(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_ewb(const Ctx& c, const pword* o) {
   constexpr int NT = NW * 64;
   const int flags = o[O_FLAGS];
   const int C = slot_w(c, o[O_OUT], S_C);
@@ -569,7 +569,7 @@ __device__ __forceinline__ void op_ewb(const Ctx& c, const int* o) {
 
 // OP_LNB: LayerNorm backward, one wave per row
 template <int NW>
-__device__ __forceinline__ void op_lnb(const Ctx& c, const int* o) {
+__device__ __forceinline__ void op_lnb(const Ctx& c, const pword* o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int C = slot_w(c, o[O_A], S_C);
   const int x_off = slot_w(c, o[O_A], S_OFF), x_st = slot_w(c, o[O_A], S_STRIDE);
@@ -626,7 +626,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
   if (!SPLIT && args.guard && __hip_atomic_load(args.guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.epoch) return;
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   constexpr int NT = NW * 64;
-  const int* prog = args.prog;
+  const pword* prog = (const pword*)args.prog;
   const int T = prog[H_T];
   const int mode = prog[H_MODE];
   const bool train = mode == MODE_TRAIN;
@@ -663,7 +663,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
   const int in_off = slot_w(c, in_slot, S_OFF), in_st = slot_w(c, in_slot, S_STRIDE);
   const int64_t ntiles = (args.nrows + T - 1) / T;
   const bool small = args.nrows < ((int64_t)1 << 31);
-  const int* blk = prog + prog[H_BLK_OFF] + (args.pass * NW + wave) * MAXACC;
+  const pword* blk = prog + prog[H_BLK_OFF] + (args.pass * NW + wave) * MAXACC;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     c.row0 = tile * T;
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     }
     __syncthreads();
     for (int oi = 0; oi < nops; ++oi) {
-      const int* o = prog + ops_off + oi * O_WORDS;
+      const pword* o = prog + ops_off + oi * O_WORDS;
       const int type = o[O_TYPE];
       switch (type) {
         case OP_DENSE:
@@ -800,7 +800,7 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
     for (int s = 0; s < MAXACC; ++s) {
       const int ent = blk[s];
       if (ent >= 0) {
-        const int* o = prog + ops_off + (ent >> 16) * O_WORDS;
+        const pword* o = prog + ops_off + (ent >> 16) * O_WORDS;
         const int K = o[O_K], N = o[O_N], woff = o[O_W];
         const int kb = (ent >> 8) & 0xff, nb = ent & 0xff;
         const int n = nb * 32 + l32;
@@ -814,12 +814,12 @@ __global__ void __launch_bounds__(NW * 64) rowprog_kernel(Args args) {
       }
     }
     const int ntacc = prog[H_NTACC];
-    const int* tl = prog + prog[H_TACC_OFF];
+    const pword* tl = prog + prog[H_TACC_OFF];
 #pragma unroll
     for (int s = 0; s < MAXTHIN; ++s) {
       const int e = threadIdx.x + s * NT;
       for (int q = 0; q < ntacc; ++q) {
-        const int* o = prog + ops_off + tl[q] * O_WORDS;
+        const pword* o = prog + ops_off + tl[q] * O_WORDS;
         const int el = e - o[O_TBASE];
         if (el >= 0 && el < o[O_TCOUNT]) ws[o[O_W] + el] = tacc[s];
       }
