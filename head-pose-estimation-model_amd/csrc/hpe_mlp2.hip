@@ -95,7 +95,7 @@ __device__ __forceinline__ float e_bwd(const E2& e, uint64_t seed, int64_t img, 
 // the only wait in here never drains an in-flight prefetch.
 __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* lab, int64_t row0,
                                            const TileImg& ti, int wave, int NCB, int lane, int Cin,
-                                           bool labels) {
+                                           bool labels, int XS = MLP2_XS) {
   const int64_t rem = args.nrows - 1 - row0;
   const int last = rem < 31 ? (int)rem : 31;
   const int P = args.P;
@@ -112,7 +112,7 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
     }
     for (int r = wave; r < 32; r += NCB) {
       const int64_t srow = row0 + min(r, last);
-      if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
+      if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * XS));
     }
     return;
   }
@@ -136,7 +136,7 @@ __device__ __forceinline__ void stage_tile(const Args& args, float* xs, float* l
     const int rr = min(r, last);
     const int64_t srow = (int64_t)__builtin_amdgcn_readlane(lsrc, rr) * P +
                          __builtin_amdgcn_readlane(lpos, rr);
-    if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * MLP2_XS));
+    if (lane < q) glds16(args.x + srow * Cin + 4 * lane, lds_addr(xs + r * XS));
   }
 }
 
@@ -732,6 +732,387 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
 #endif
 }
 
+#ifdef MLP2_BIG
+// ------------------------------------------------------------------------------------------------
+// mlp2r_kernel: the large-launch training kernel for NARROW hidden layers (F <= 64: Model-88's
+// create_model, 88 -> 64 softsign -> 3, train_88.py:66-140), one WAVE per workgroup and every wave
+// a whole worker over its own 32-row tiles.  mlp2_kernel gives such a layer two waves per tile:
+// both split the same X tile (the data-side split is most of their VALU work), they meet at three
+// barriers per tile and run two waves per SIMD at the 256-VGPR budget.  Here one wave owns all 64
+// hidden units (two 32-unit blocks: W1 as hi / lo fp16 B fragments, 96 VGPRs, and the dW1
+// accumulators, 96), so
+//   * each X tile is split once per layout and feeds both unit blocks' MFMAs;
+//   * the 3-wide head is reduced inside the wave (A1 parked in the wave's LDS, row-on-lane reads,
+//     one xor-32 exchange);
+//   * no workgroup barrier: LDS order inside one wave, and the next tile's LDS-DMA in flight over
+//     the whole compute of the current one;
+//   * one wave per SIMD (up to 512 VGPRs), four workgroups per CU (~37 KB of LDS each).
+// Same arithmetic per product as mlp2_kernel's SPLIT path (exponent-shifted 3-product fp16 split,
+// fp32 accumulation), another summation order (per wave over its tiles; the reduce kernel sums the
+// per-workgroup slabs in fixed order): deterministic, within the split's error bound.  The exact
+// twin (mlp2_kernel<KH, ACT1, DROP, 4, false>, same grid and slabs) recomputes a flagged launch.
+// ------------------------------------------------------------------------------------------------
+#define MLP2R_NU 2  // 32-unit blocks per wave (F <= 64)
+#define MLP2R_LDS_FLOATS (2 * MLP2_XF + 2 * MLP2_LAB + MLP2R_NU * MLP2_A1W + 32 * 4 + MLP2R_NU * 128 + 4)
+
+template <int KH, int ACT1, bool DROP>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) mlp2r_kernel(Args args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NU = MLP2R_NU;
+  constexpr int NKB = (2 * KH + 31) / 32;
+  constexpr int T = 32;
+  // Cin = 88: X tiles packed at the row stride 88 (11264 B = 11 full 64-lane LDS-DMA pieces per
+  // tile instead of 32 one-row pieces: the piece issue cost was a fifth of the tile's cycles);
+  // the forward's b128 reads take 2-way bank conflicts there.  Cin = 96 keeps the padded stride.
+  constexpr int XS = KH == 44 ? 88 : MLP2_XS;
+  const int* prog = args.prog;
+  const int* o = prog + prog[H_OPS_OFF];
+  const int Cin = o[O_K], F = o[O_N];
+  const int lane = threadIdx.x, half = lane >> 5, l32 = lane & 31;
+  float* xbuf = lds;                  // [2][MLP2_XF]: X tiles [32][XS] (double-buffered LDS-DMA)
+  float* lbuf = xbuf + 2 * MLP2_XF;   // [2][32][4] labels
+  float* a1p = lbuf + 2 * MLP2_LAB;   // [NU][MLP2_A1W] A1 park (a1_row slots)
+  float* dz2 = a1p + NU * MLP2_A1W;   // [32][4] output gradients of the tile
+  float* w2t = dz2 + 32 * 4;          // [NU * 32][4] W2 rows (zero past F)
+  float* b2t = w2t + NU * 128;        // [4]
+  const E2 e1 = {o[O_EACT], o[O_EDROP], (uint32_t)o[O_ETHR], __int_as_float(o[O_EKEEP])};
+  const E2 e2 = {o[O_AUX2], o[O_TBASE], (uint32_t)o[O_TCOUNT], __int_as_float(o[O_F0])};
+  const float inv_keep1 = 1.f / e1.keep, inv_keep2 = 1.f / e2.keep;
+  const float* W1 = args.params + o[O_W];
+  const float* W2 = args.params + o[O_AUX0];
+  const int o_bias = __builtin_amdgcn_readfirstlane(o[O_BIAS]), o_aux1 = __builtin_amdgcn_readfirstlane(o[O_AUX1]);
+
+  const int64_t nrows = args.nrows;
+  const int64_t ntiles = (nrows + T - 1) / T;
+  const int P = args.P;
+  const int S = gridDim.x * T, dq = S / P, dr = S - dq * P;
+  TileImg ti;
+  ti.P = P;
+  ti.img0 = (int)(blockIdx.x * T / P);
+  ti.rem0 = (int)(blockIdx.x * T - ti.img0 * P);
+  auto stage = [&](float* xd, float* ld, int64_t r0, const TileImg& t) {
+    if (XS == 88 && !args.idx && P >= 32 && r0 + T <= nrows && Cin == 88) {
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int slot = pc * 64 + lane;
+        glds4(args.ytrue + (int64_t)t.of(slot >> 2) * 3 + min(slot & 3, 2), lds_addr(ld + pc * 64));
+      }
+#pragma unroll
+      for (int i = 0; i < 11; ++i) glds16(args.x + r0 * 88 + 256 * i + 4 * lane, lds_addr(xd + 256 * i));
+    } else {
+      stage_tile(args, xd, ld, r0, t, 0, 1, lane, Cin, true, XS);
+    }
+  };
+  if (blockIdx.x < ntiles) stage(xbuf, lbuf, (int64_t)blockIdx.x * T, ti);
+
+  // ---- this wave's hidden units n = 32 u + l32: W1 columns split in registers, per-unit scalars ----
+  SplitW wsp[NU][6];
+  float inv1[NU], b1v[NU], s2[NU], nm[NU];  // nm: 1 for a unit below F, 0 past it (branch-free masks)
+  f32x4 w2v[NU];
+  bool nok[NU];
+  {
+    f32x8 v[NU][6];
+    float w2r[NU][3], b1r[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int n = 32 * u + l32, nc = min(n, F - 1);
+      nok[u] = n < F;
+      nm[u] = nok[u] ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) w2r[u][j] = W2[nc * 3 + j];
+      b1r[u] = args.params[max(o_bias, 0) + nc];
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = half * KH + 8 * s + j;
+          v[u][s][j] = 8 * s + j < KH ? W1[(size_t)min(k, Cin - 1) * F + nc] : 0.f;
+        }
+      }
+    }
+    const float b2r = args.params[max(o_aux1, 0) + min(lane & 3, 2)];
+    __builtin_amdgcn_sched_barrier(0);  // every prologue load in flight before the first use
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      float mx = 0.f;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = half * KH + 8 * s + j;
+          v[u][s][j] = (k < Cin && nok[u]) ? v[u][s][j] : 0.f;
+          mx = fmaxf(mx, fabsf(v[u][s][j]));
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float s1 = pow2_scale(mx, 13);
+      inv1[u] = SPLIT_INV_C / s1;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) wsp[u][s] = split_w8(v[u][s] * s1);
+      w2v[u] = nok[u] ? f32x4{w2r[u][0], w2r[u][1], w2r[u][2], 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+      s2[u] = pow2_scale(nok[u] ? fmaxf(fmaxf(fabsf(w2r[u][0]), fabsf(w2r[u][1])), fabsf(w2r[u][2])) : 0.f, 2);
+      b1v[u] = (nok[u] && o_bias >= 0) ? b1r[u] : 0.f;
+      if (half == 0) *(f32x4*)(w2t + (32 * u + l32) * 4) = w2v[u];
+    }
+    if (lane < 4) b2t[lane] = (lane < 3 && o_aux1 >= 0) ? b2r : 0.f;
+  }
+  // pad columns [C_in, 96) of both X buffers: read by the forward (against zero weights) and by the
+  // dW1 blocks past C_in (never flushed) -> zeros, not stale LDS (the DMA writes [0, C_in))
+  if (XS == 88) {
+    // packed rows: the reads past channel 88 land in the next row (finite, against zero weights /
+    // unflushed dW1 rows) and, for the last row, in the tile buffer's tail: zeros
+    for (int i = lane; i < 2 * (MLP2_XF - 32 * 88); i += 64)
+      xbuf[(i >= MLP2_XF - 32 * 88 ? MLP2_XF : 0) + 32 * 88 + i % (MLP2_XF - 32 * 88)] = 0.f;
+  } else {
+    for (int i = lane; i < 2 * 32 * 16; i += 64) {
+      const int r = i >> 4, c = Cin + (i & 15);
+      if (c < 96) xbuf[r * MLP2_XS + c] = 0.f;
+    }
+  }
+
+  f32x16 dw[NU][NKB];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) dw[u][kb] = f32x16{};
+  float dw2[NU][3], db1[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) { dw2[u][0] = dw2[u][1] = dw2[u][2] = 0.f; db1[u] = 0.f; }
+  float sse = 0.f, sae = 0.f, db2[3] = {0.f, 0.f, 0.f};
+  bool bad = false;
+
+  int buf = 0;
+#ifdef MLP2R_STAMPS
+  uint32_t ph[7] = {};
+  uint64_t tprev = __builtin_amdgcn_s_memtime();
+#define RSTAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[i] += (uint32_t)(t_ - tprev); tprev = t_; } while (0)
+#else
+#define RSTAMP(i) do {} while (0)
+#endif
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, buf ^= 1, ti.advance(dq, dr)) {
+    const int64_t row0 = tile * T;
+    RSTAMP(0);
+    // tile `tile` landed; nothing else in flight -> the other buffer (read by the previous tile, all
+    // of whose reads have returned) takes the next tile's LDS-DMA
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tile + gridDim.x < ntiles) {
+      TileImg tn = ti;
+      tn.advance(dq, dr);
+      stage(xbuf + (buf ^ 1) * MLP2_XF, lbuf + (buf ^ 1) * MLP2_LAB, (tile + gridDim.x) * T, tn);
+    }
+    const float* xs = xbuf + buf * MLP2_XF;
+    const float* lab = lbuf + buf * MLP2_LAB;
+    RSTAMP(1);
+
+    // ---- forward: Z1 = X.W1 for both unit blocks off one split of each X K-step ----
+    f32x16 acc[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc[u] = f32x16{};
+    {
+      // one wave per SIMD: nothing hides a load's latency but the wave's own other work, so every
+      // read of a phase is issued before its first use (here: the tile's 12 X reads, then split +
+      // MFMA per K-step as they land)
+      const float* ap = xs + l32 * XS + half * KH;
+      f32x4 xa[12];
+#pragma unroll
+      for (int s = 0; s < 12; ++s) xa[s] = *(const f32x4*)(ap + 4 * s);
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const f32x4 a0 = xa[2 * s], a1 = xa[2 * s + 1];
+        const SplitD xd = split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w});
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[u] = mfma3_dw(xd, wsp[u][s], acc[u]);
+      }
+    }
+    RSTAMP(2);
+    uint32_t dmask[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      bad |= !(fabsf(sum16(acc[u])) <= 3.0e38f);
+      const int n = 32 * u + l32;
+      dmask[u] = 0u;
+      if (DROP) {
+        if (P >= 32) {
+          const bool k0 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + args.img_off), n) >= e1.thr;
+          const bool k1 = drop_hash(args.seed, e1.drop, (uint64_t)(ti.img0 + 1 + args.img_off), n) >= e1.thr;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask[u] |= (ti.rem0 + r >= P ? k1 : k0) ? (1u << g) : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int r = (g & 3) + 8 * (g >> 2) + 4 * half;
+            dmask[u] |= drop_hash(args.seed, e1.drop, (uint64_t)(ti.of(r) + args.img_off), n) >= e1.thr ? (1u << g) : 0u;
+          }
+        }
+      }
+      // multiplies by 0 / 1 / inv_keep instead of selects: the compiler turns value selects over
+      // several instructions into per-element branches, each behind its own LDS wait
+      // A1 stays in acc for the backward; the park is for the head's row-on-lane reads
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float km = DROP ? ((dmask[u] >> g) & 1u ? inv_keep1 : 0.f) : 1.f;
+        acc[u][g] = act1_f<ACT1>(e1.act, fmaf(acc[u][g], inv1[u], b1v[u])) * km * nm[u];
+        a1p[u * MLP2_A1W + a1_row(g) + lane] = acc[u][g];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    RSTAMP(3);
+    // ---- head in the wave: lane (row r, half h) dots A1[r][32 u + 16 h ..] with the W2 rows ----
+    {
+      const int r = l32, hh = (r >> 2) & 1, gr = (r & 3) + 4 * (r >> 3);
+      const f32x4 lv = *(const f32x4*)(lab + r * 4);
+      float h0 = 0.f, h1 = 0.f, h2 = 0.f;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const float* ar = a1p + u * MLP2_A1W + a1_row(gr) + hh * 32 + 16 * half;
+        const float* wr = w2t + (32 * u + 16 * half) * 4;
+        f32x4 av[4], wv[16];  // the block's 20 reads in flight together
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)(ar + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wv[i] = *(const f32x4*)(wr + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          h0 = fmaf(av[i >> 2][i & 3], wv[i].x, h0);
+          h1 = fmaf(av[i >> 2][i & 3], wv[i].y, h1);
+          h2 = fmaf(av[i >> 2][i & 3], wv[i].z, h2);
+        }
+      }
+      h0 += __shfl_xor(h0, 32, 64);
+      h1 += __shfl_xor(h1, 32, 64);
+      h2 += __shfl_xor(h2, 32, 64);
+      if (half == 0) {
+        const bool valid = row0 + r < nrows;
+        const bool d2 = __builtin_expect(e2.drop >= 0, 0);
+        const int64_t img = d2 ? ti.of(r) + args.img_off : 0;
+        const float zs[3] = {b2t[0] + h0, b2t[1] + h1, b2t[2] + h2};
+        float gs[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const bool k2 = d2 ? drop_hash(args.seed, e2.drop, (uint64_t)img, j) >= e2.thr : true;
+          const float kk = d2 ? (k2 ? inv_keep2 : 0.f) : 1.f;
+          const float p = zs[j] * kk;
+          float g = 0.f;
+          if (valid) {
+            const float err = p - lv[j];
+            sse = fmaf(err, err, sse);
+            sae += fabsf(err);
+            g = 2.f * err;
+          }
+          g *= kk;
+          db2[j] += g;
+          gs[j] = g;
+        }
+        *(f32x4*)(dz2 + r * 4) = f32x4{gs[0], gs[1], gs[2], 0.f};
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    RSTAMP(4);
+    // ---- backward: dZ1 per unit block (registers), dW2 / db1, dW1 += X^T.dZ1 off one X^T split ----
+    // the 16 rows' dZ2 of this lane's half and the tile's X^T reads (both K-steps), all in flight
+    f32x4 dzr[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dzr[g] = *(const f32x4*)(dz2 + ((g & 3) + 8 * (g >> 2) + 4 * half) * 4);
+    f32x8 xtr[2][NKB];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          xtr[s][kb][j] = xs[(4 * half + 16 * s + 8 * (j >> 2) + (j & 3)) * XS + kb * 32 + l32];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f32x8 dv[NU];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int g = 8 * s + j;
+        const f32x4 d = dzr[g];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const float a = acc[u][g];
+          const float da = d.x * w2v[u].x + d.y * w2v[u].y + d.z * w2v[u].z;
+          const float km = DROP ? ((dmask[u] >> g) & 1u ? inv_keep1 : 0.f) : 1.f;
+          const float gz = da * km * act1_g<ACT1>(e1.act, DROP ? a * e1.keep : a) * nm[u];
+          dw2[u][0] = fmaf(a, d.x, dw2[u][0]);
+          dw2[u][1] = fmaf(a, d.y, dw2[u][1]);
+          dw2[u][2] = fmaf(a, d.z, dw2[u][2]);
+          db1[u] += gz;
+          dv[u][j] = gz;
+        }
+      }
+      SplitW dsp[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) dsp[u] = split_w8(dv[u] * s2[u]);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        const SplitD xd = split_d8(xtr[s][kb]);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) dw[u][kb] = mfma3_dw(xd, dsp[u], dw[u][kb]);
+      }
+      if (s == 0) RSTAMP(5);
+    }
+    RSTAMP(6);
+  }
+#ifdef MLP2R_STAMPS
+  if (blockIdx.x < 2 && lane == 0)
+    printf("RSTAMP wg %d top %u stage %u fwd %u act %u head %u bwd0 %u bwd1 %u\n", (int)blockIdx.x, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+#endif
+
+  // ---- flush this workgroup's partial gradients + loss sums (mlp2_kernel's slab layout) ----
+  const int slab = prog[H_SLAB];
+  const int npt = prog[H_NPARAMS_TRAIN];
+  float* ws = args.ws + (size_t)blockIdx.x * slab;
+  const float sc = args.inv_count;
+  const int oW = __builtin_amdgcn_readfirstlane(o[O_W]), oA0 = __builtin_amdgcn_readfirstlane(o[O_AUX0]);
+  float chk = 0.f;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int n = 32 * u + l32;
+    const float scw = sc * (SPLIT_INV_C / s2[u]);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      chk += sum16(dw[u][kb]);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int k = kb * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+        if (k < Cin && nok[u]) ws[oW + (size_t)k * F + n] = dw[u][kb][g] * scw;
+      }
+    }
+    const float tb = db1[u] + __shfl_xor(db1[u], 32, 64);
+    float t2[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) t2[j] = dw2[u][j] + __shfl_xor(dw2[u][j], 32, 64);
+    if (half == 0 && nok[u]) {
+      if (o_bias >= 0) ws[o_bias + n] = tb * sc;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ws[oA0 + n * 3 + j] = t2[j] * sc;
+    }
+  }
+  bad |= !(fabsf(chk) <= 3.0e38f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float t = wave_sum(db2[j]);
+    if (lane == 0 && o_aux1 >= 0) ws[o_aux1 + j] = t * sc;
+  }
+  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float ta = wave_sum(sse), tb = wave_sum(sae);
+  if (lane == 0) {
+    ws[npt] = ta;
+    ws[npt + 1] = tb;
+  }
+}
+#endif
+
 // ---- host-side dispatch ---------------------------------------------------------------------
 typedef void (*mlp2_fn)(Args);
 
@@ -799,6 +1180,30 @@ static bool split_only() {
   return e && e[0] == '1';
 }
 
+#ifdef MLP2_BIG
+// the row-parallel split kernel for this training program, or null: F <= 64, linear head, layer-1
+// activation compiled in; HPE_MLP2_ROWS=0 keeps mlp2_kernel (A/B, tests)
+template <int KH>
+static mlp2_fn pick_r_act(int act, bool drop) {
+  if (act == ACT_TANH) return drop ? mlp2r_kernel<KH, ACT_TANH, true> : mlp2r_kernel<KH, ACT_TANH, false>;
+  if (act == ACT_SOFTSIGN) return drop ? mlp2r_kernel<KH, ACT_SOFTSIGN, true> : mlp2r_kernel<KH, ACT_SOFTSIGN, false>;
+  return nullptr;
+}
+static mlp2_fn pick_r(const int* w) {
+  const char* e = getenv("HPE_MLP2_ROWS");
+  if ((e && e[0] == '0') || w[H_MODE] != MODE_TRAIN) return nullptr;
+  const int* o = w + w[H_OPS_OFF];
+  if (o[O_MODE] > MLP2R_NU || o[O_N] > 32 * MLP2R_NU || o[O_AUX2] != ACT_LINEAR) return nullptr;
+  const int kh = ((o[O_K] + 7) & ~7) / 2;
+  if (kh == 44 && o[O_K] == 88) return pick_r_act<44>(o[O_EACT], o[O_EDROP] >= 0);  // packed 88-float rows
+  if (kh == 48) return pick_r_act<48>(o[O_EACT], o[O_EDROP] >= 0);
+  return nullptr;
+}
+#else
+static mlp2_fn pick_r(const int*) { return nullptr; }
+#define MLP2R_LDS_FLOATS 0
+#endif
+
 // split instantiation, then the exact one, which exits at once unless the split launch flagged a
 // non-finite value (guard == epoch); hpe_set_exact_fp32(1): the exact kernel alone
 static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
@@ -812,8 +1217,9 @@ static int launch_pair(const int* w, const Args& a, int grid, hipStream_t s) {
     hpe_tev_end(s, tv);
     return rc;
   }
+  const mlp2_fn kr = pick_r(w);
   const int tv = hpe_tev_begin(s);
-  const int rc = launch_k(pick(w, true), ncb, lds_split(w), a, grid, s);
+  const int rc = kr ? launch_k(kr, 1, MLP2R_LDS_FLOATS * 4, a, grid, s) : launch_k(pick(w, true), ncb, lds_split(w), a, grid, s);
   hpe_tev_end(s, tv);
   if (rc) return rc;
   if (split_only()) return 0;
@@ -842,7 +1248,9 @@ static int cap_per_cu(const int* w) {
   int kh, rbw, ncb, lds, act, drop;
   geom(w, kh, rbw, ncb, lds, act, drop);
   const int a = per_cu_of(pick(w), ncb, lds), b = per_cu_of(pick(w, true), ncb, lds_split(w));
-  return a < b ? a : b;
+  const mlp2_fn kr = pick_r(w);
+  const int c = kr ? per_cu_of(kr, 1, MLP2R_LDS_FLOATS * 4) : b;
+  return a < b ? (a < c ? a : c) : (b < c ? b : c);
 }
 }  // namespace MLP2_NS
 

@@ -414,6 +414,78 @@ def test_train_step_repeatable(rid, side, n, R):
         assert np.array_equal(g, ref), 'run %d differs from run 0 in %d entries' % (r, int((g != ref).sum()))
 
 
+@pytest.mark.parametrize('F,act,dropout,cin,side,n', [(64, 'softsign', 0.2, 88, 88, 8), (64, 'tanh', 0.0, 96, 87, 5),
+                                                      (40, 'softsign', 0.3, 88, 64, 10), (64, 'softsign', 1e-4, 88, 88, 6)])
+def test_train_step_rows_kernel(F, act, dropout, cin, side, n):
+    """The row-parallel split training kernel for narrow hidden layers (csrc/hpe_mlp2.hip
+    mlp2r_kernel: F <= 64, launches of >= 2^15 rows, train_88.py:66-140's 88 -> 64 softsign -> 3)
+    against the exact-fp32 kernel and the float64 oracle (same bars as the 12-wave kernel's test),
+    against the unit-split kernel it replaces (HPE_MLP2_ROWS=0: same products, another summation
+    order), ragged rows (87 x 87 maps), F < 64, dropout on both layers; then the guard: a feature
+    beyond the split's data range hands the launch to the exact twin."""
+    from hpe import _lib
+    hpe.set_seed(F + cin)
+    keras.backend.clear_session()
+    reg = keras.regularizers.l2(1e-6)
+    inp = keras.Input(shape=(None, None, cin))
+    h = keras.layers.Conv2D(F, 1, padding='same', activation=act, kernel_regularizer=reg)(inp)
+    h = keras.layers.SpatialDropout2D(dropout)(h)
+    o = keras.layers.Conv2D(3, 1, padding='same', kernel_regularizer=reg)(h)
+    o = keras.layers.SpatialDropout2D(dropout)(o)
+    m = keras.Model(inp, o)
+    m.compile(optimizer=keras.optimizers.Adam(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    mc, w = m.model_config, m.weights_dict()
+    eng = m._eng()
+    P = side * side
+    assert eng.program('train', P).prog.kind == 'mlp2' and n * P >= 1 << 15
+    x = features(n, cin, seed=F + 3, h=side, w=side)
+    y = labels(n, seed=F + 4)
+    xt = torch.from_numpy(x.reshape(n * P, cin)).cuda()
+    yt = torch.from_numpy(y.reshape(n, 3).astype(np.float32)).cuda()
+    inv = 1.0 / (n * P * 3)
+
+    def grad(xd):
+        return eng.gradient(xd, yt, P, None, n, inv, seed=5).cpu().numpy().copy()
+
+    lib = _lib.load()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        g_exact = grad(xt)
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    g_rows = grad(xt)
+    os.environ['HPE_MLP2_ROWS'] = '0'
+    try:
+        g_units = grad(xt)
+    finally:
+        del os.environ['HPE_MLP2_ROWS']
+    assert not np.array_equal(g_rows, g_units)  # the two kernels ran (different summation orders)
+    npt = eng.n_train
+    g64 = _data_grad64(mc, w, x, y, eng.layout, 5)
+    scale = np.abs(g64).max()
+    e_exact = np.abs(g_exact[:npt] - g64).max() / scale
+    e_rows = np.abs(g_rows[:npt] - g64).max() / scale
+    e_units = np.abs(g_units[:npt] - g64).max() / scale
+    d = np.abs(g_rows[:npt] - g_exact[:npt]).max() / scale
+    print('F=%d %s drop %g cin %d P=%d: vs float64 exact %.2e rows %.2e units %.2e; |rows - exact| / max|g| = %.2e'
+          % (F, act, dropout, cin, P, e_exact, e_rows, e_units, d))
+    assert e_rows <= 4 * e_exact + 2.0 ** -24, (e_rows, e_exact)
+    assert d <= 1e-6, d
+    np.testing.assert_allclose(g_rows[npt:npt + 2], g_exact[npt:npt + 2], rtol=1e-5)
+    np.testing.assert_allclose(g_rows[npt:npt + 2], g_units[npt:npt + 2], rtol=1e-5)
+    xo = x.reshape(n * P, cin).copy()
+    xo[(n * P) // 2 + 1, 7] = 100.0
+    xot = torch.from_numpy(xo).cuda()
+    prev = lib.hpe_set_exact_fp32(1)
+    try:
+        go_exact = grad(xot)
+    finally:
+        lib.hpe_set_exact_fp32(prev)
+    go = grad(xot)
+    assert np.isfinite(go).all()
+    np.testing.assert_array_equal(go, go_exact)
+
+
 def _create_model(F, act, dropout, l2, lr=2.8e-4):
     """train_96.py:65-110 create_model with the given width / activation / rates."""
     keras.backend.clear_session()
