@@ -1,4 +1,6 @@
-"""Bank-conflict model of the 12-wave mlp2_kernel's LDS layouts (csrc/hpe_mlp2.hip).
+"""Bank-conflict model of the training kernels' LDS layouts (csrc/hpe_mlp2.hip): the 12-wave
+mlp2_kernel, the 4-wave mlp2_kernel (narrow layers at P < 2^15 rows, the split path that splits X
+per wave) and mlp2r_kernel (F <= 64, large launches).
 
 The lane groups and bank rules are MI355X_MICROARCH.md §LDS's table: ds_read_b128 serves a wave in
 four 16-lane groups, bank of dword d = d mod 64, one LDS cycle per group when every bank holds at
@@ -72,3 +74,56 @@ def test_transposed_image_reads_conflict_free(kb, step):
     addr = {lane: ((lane & 31) * MLP2_TS + 8 * (lane >> 5) + 16 * step + kb * 32 * MLP2_TS) // 2
             for lane in range(64)}
     assert cycles(addr, B128_GROUPS, 4, 64) == 4
+
+
+MLP2_XS = 100   # floats per row of the raw X tile (the 4-wave kernel and mlp2r at C_in = 96)
+
+
+@pytest.mark.parametrize('kh,s', [(kh, s) for kh in (44, 48) for s in range(12)])
+def test_four_wave_forward_reads_conflict_free(kh, s):
+    # ap = xs + l32 MLP2_XS + half KH, + 4 s (two b128 per K-step: 8 s and 8 s + 4)
+    addr = {lane: (lane & 31) * MLP2_XS + (lane >> 5) * kh + 4 * s for lane in range(64)}
+    assert cycles(addr, B128_GROUPS, 4, 64) == 4
+
+
+@pytest.mark.parametrize('xs', [MLP2_XS, 88])
+def test_transposed_b32_reads_conflict_free(xs):
+    # dW1 K-step s, block kb: lane reads X[4 half + 16 s + 8 (j >> 2) + (j & 3)][32 kb + l32]
+    for kb in range(3):
+        for s in range(2):
+            for j in range(8):
+                addr = {lane: (4 * (lane >> 5) + 16 * s + 8 * (j >> 2) + (j & 3)) * xs + 32 * kb + (lane & 31)
+                        for lane in range(64)}
+                assert cycles(addr, B32_GROUPS, 1, 32) == 2
+
+
+def test_rows_kernel_packed_rows_cost_two_way_forward_reads():
+    # mlp2r at C_in = 88: rows packed at stride 88 (11 full LDS-DMA pieces per tile instead of 32
+    # one-row pieces); the forward's b128 reads become 2-way (8 cycles instead of 4, 12 reads per
+    # tile: +48 LDS cycles against ~2.5 k cycles of DMA issue saved, measured 0.875 -> 0.797 ms)
+    for s in range(12):
+        addr = {lane: (lane & 31) * 88 + (lane >> 5) * 44 + 4 * s for lane in range(64)}
+        assert cycles(addr, B128_GROUPS, 4, 64) == 8
+
+
+def test_rows_kernel_broadcast_reads():
+    # the head's W2 rows (w2t + (32 u + 16 h + i) 4) and the backward's dZ2 rows (dz2 + r(g) 4):
+    # one address per half-wave, one LDS cycle per lane group
+    for u in range(2):
+        for i in range(16):
+            addr = {lane: (32 * u + 16 * (lane >> 5) + i) * 4 for lane in range(64)}
+            assert cycles(addr, B128_GROUPS, 4, 64) == 4
+    for g in range(16):
+        addr = {lane: ((g & 3) + 8 * (g >> 2) + 4 * (lane >> 5)) * 4 for lane in range(64)}
+        assert cycles(addr, B128_GROUPS, 4, 64) == 4
+
+
+def test_unit_split_head_reads():
+    # mlp2_kernel's head: thread it sums part[(w T + r) 4 + j], r = it / 3, j = it % 3 (b32);
+    # rows 8.. of the first 32 lanes wrap onto banks 0.. (2-way: 4 cycles on the first wave), the
+    # per-thread loss accumulators hacc[tid HS + k] (HS = 3 on the 4-wave kernel) are conflict-free
+    first = {lane: 4 * (lane // 3) + lane % 3 for lane in range(64)}
+    assert cycles(first, B32_GROUPS, 1, 32) == 4
+    second = {lane: 4 * ((64 + lane) // 3) + (64 + lane) % 3 for lane in range(32)}
+    assert cycles(second, [list(range(32))], 1, 32) == 2
+    assert cycles({lane: 3 * lane for lane in range(64)}, B32_GROUPS, 1, 32) == 2
