@@ -250,9 +250,11 @@ def run_train(eng, opt, x, y, P, n_local, n_global, rank, world, steps, warmup, 
     return dt, kms, mse, kt.mean()
 
 
-def train_kernel_name(eng, P):
-    """The kernel libhpe.so runs for a training launch of this program (csrc/hpe_mlp2.hip
-    launch_pair: mlp2_kernel, its fp16-split instantiation unless exact fp32 is forced)."""
+def train_kernel_name(eng, P, rows=0):
+    """The kernel libhpe.so runs for a training launch of this program over `rows` rows
+    (csrc/hpe_mlp2.hip launch_pair / pick_r: the row-parallel mlp2r_kernel for F <= 64 on launches of
+    >= 2^15 rows, else mlp2_kernel; the fp16-split instantiations unless exact fp32 is forced)."""
+    from hpe.compiler import ACTS
     prog = eng.program('train', P).prog
     if prog.kind == 'res':
         return 'res_train_kernel'
@@ -260,6 +262,10 @@ def train_kernel_name(eng, P):
         return 'rowprog_kernel'
     if os.environ.get('HPE_EXACT_FP32') == '1':
         return 'mlp2_kernel (exact fp32)'
+    i = prog.info
+    if (os.environ.get('HPE_MLP2_ROWS') != '0' and rows >= 1 << 15 and i['F'] <= 64 and i['act2'] == 0 and
+            i['act'] in (ACTS['tanh'], ACTS['softsign']) and (i['cin'] == 88 or (i['cin'] + 7) // 8 * 4 == 48)):
+        return 'mlp2r_kernel'
     return 'mlp2_kernel'
 
 
@@ -521,7 +527,7 @@ def bench_train88(hpe, keras, dev, steps, warmup):
     return {'workload': 'Model-88 create_model (88-64 softsign-3, dropout 1e-4, l2 1e-6) training, legacy Adam, '
                         '512 images of 88x88 feature maps',
             'value': n * steps / dt, 'unit': 'images/sec', 'ms_per_step': dt * 1e3 / steps, 'dtype': 'fp32',
-            'kernel': train_kernel_name(eng, Pm),
+            'kernel': train_kernel_name(eng, Pm, n * Pm),
             'roofline': {'bound': 'mfma', 'achieved': ach / 1e12, 'peak': gemm_peak()[0] / 1e12, 'unit': 'TFLOP/s',
                          'frac': ach / gemm_peak()[0], 'gemm': gemm_peak()[1], 'traffic': _traffic('train88'),
                          'dominant_kernel_ms': dom_ms, 'step_kernels_ms': kms, 'flop_per_launch': flop * n * Pm}}
@@ -781,7 +787,7 @@ def main(argv=None):
             'roofline': {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': gemm_peak()[0] / 1e12,
                          'unit': 'TFLOP/s', 'frac': achieved / gemm_peak()[0], 'gemm': gemm_peak()[1],
                          'traffic': _traffic('train'),
-                         'kernel': train_kernel_name(eng, P),
+                         'kernel': train_kernel_name(eng, P, PER_GPU * P),
                          'dominant_kernel_ms': dom_ms,
                          'frac_from': 'flop_per_launch / dominant_kernel_ms (HIP events around the dominant '
                                       'kernel alone, every timed step, on the launch stream) / peak',

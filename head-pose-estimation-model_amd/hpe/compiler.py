@@ -1040,7 +1040,7 @@ def _try_mlp2(b, x_t, y_t, mode, n_train, l2c, P, rbw=1):
         op[O_F0] = _f2i(np.float32(1.0) - np.float32(f2.rate))
     op[O_FLAGS], op[O_MODE] = rbw, ncb
     return _fused_program(b, op, 1, 32 * rbw, ncb, mode, n_train, l2c, cin,
-                          {'kind': 'mlp2', 'F': F, 'waves': ncb})
+                          {'kind': 'mlp2', 'F': F, 'waves': ncb, 'cin': cin, 'act': f1.act, 'act2': f2.act})
 
 
 RES_NB = (1, 2, 3, 4)    # residual blocks the fused residual-stack kernel is instantiated for
