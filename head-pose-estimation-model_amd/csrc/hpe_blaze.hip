@@ -732,7 +732,17 @@ __device__ __forceinline__ void bfs_wstore(const BfSub& o, const f32x4 (&pf)[BFS
 // output-channel chunk grp * nc + j at the 32 positions of chunk `chunk`; src = the input map
 // (global: the stage input of this image, channel stride cinp; LDS: the resident map, stride cs)
 #define BFS_MAXNC 3  // output-channel chunks per wave task (acc registers: 16 each)
-template <bool G, bool DW, int RES>
+// DPP (stride-1 depthwise ops on 16- or 8-wide maps from the LDS map): per 3x3 row one ds_read_b128
+// of the centre column, the x-neighbours by DPP row shifts of it (a 16-lane DPP row is one 16-wide
+// map row or two 8-wide ones; lanes whose neighbour is across a map-row edge are zeroed by the tap
+// mask as before): 3 tap reads per K-step instead of 9, the same FMAs in the same order (bit-identical)
+__device__ __forceinline__ float dpp_from_prev(float v) {  // lane i <- lane i - 1 of its 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float dpp_from_next(float v) {  // lane i <- lane i + 1 of its 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));
+}
+template <bool G, bool DW, int RES, bool DPP = false>
 __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int ss, const float* wt,
                                          const float* dwt, const float* P_, int chunk, int grp,
                                          f32x16 (&acc)[BFS_MAXNC]) {
@@ -764,8 +774,21 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
     f32x4 av;
     if (DW) {
       f32x4 xv[9];
+      if (DPP) {
 #pragma unroll
-      for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(src + toff[tp] + c0);
+        for (int dy = 0; dy < 3; ++dy) {
+          const f32x4 c = ld4(src + toff[3 * dy + 1] + c0);
+          xv[3 * dy + 1] = c;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xv[3 * dy][e] = dpp_from_prev(c[e]);
+            xv[3 * dy + 2][e] = dpp_from_next(c[e]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(src + toff[tp] + c0);
+      }
       av = ld4(dwt + 9 * cinp + c0);
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) {
@@ -843,6 +866,8 @@ __global__ void __launch_bounds__(BFS_NW * 64) bf_stage_kernel(BfStageArgs a) {
         bfs_task<false, false, BF_RES_NONE>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
       } else if (o.res == BF_RES_MAXPOOL) {
         bfs_task<false, true, BF_RES_MAXPOOL>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+      } else if (o.s == 1 && o.res == BF_RES_ID && (o.wo == 16 || o.wo == 8) && o.w == o.wo && o.padl == 1) {
+        bfs_task<false, true, BF_RES_ID, true>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
       } else {
         bfs_task<false, true, BF_RES_ID>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
       }
