@@ -499,6 +499,15 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       float pv[MLP2_MAXW];  // all partial loads in flight, summed in fixed wave order
 #pragma unroll
       for (int w = 0; w < MLP2_MAXW; ++w) pv[w] = w < NCB ? part[(w * T + r) * 4 + j] : 0.f;
+      // the label and this thread's loss accumulators read with the partials (one LDS round trip;
+      // read-modify-written one by one behind the dz2 store they were three more on the head's path)
+      float lv = 0.f, ha0 = 0.f, ha1 = 0.f, ha2 = 0.f;
+      if (mode != MODE_FWD) {
+        lv = lab[r * 4 + j];
+        ha0 = hacc[threadIdx.x * HS + 0];
+        ha1 = hacc[threadIdx.x * HS + 1];
+        ha2 = hacc[threadIdx.x * HS + 2];
+      }
 #pragma unroll
       for (int w = 0; w < MLP2_MAXW; ++w) z += pv[w];
       // ACT1 >= 0 kernels are only picked for a linear head (the create_model family); the row's
@@ -517,16 +526,19 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       } else {
         float g = 0.f;
         if (R < nrows) {
-          const float err = p - lab[r * 4 + j];
-          hacc[threadIdx.x * HS + 0] = fmaf(err, err, hacc[threadIdx.x * HS + 0]);
-          hacc[threadIdx.x * HS + 1] += fabsf(err);
+          const float err = p - lv;
+          ha0 = fmaf(err, err, ha0);
+          ha1 += fabsf(err);
           g = SPLIT ? 2.f * err : 2.f * err * args.inv_count;
         }
         if (train) {
           g = ACT1 >= 0 ? (d2 ? (k2 ? g / e2.keep : 0.f) : g) : e_bwd(e2, args.seed, img, j, g, p);
           dz2[r * 4 + j] = g;
-          hacc[threadIdx.x * HS + 2] += g;
+          ha2 += g;
         }
+        hacc[threadIdx.x * HS + 0] = ha0;
+        hacc[threadIdx.x * HS + 1] = ha1;
+        hacc[threadIdx.x * HS + 2] = ha2;
       }
     }
     STAMP(6);
