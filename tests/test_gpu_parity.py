@@ -415,7 +415,8 @@ def test_train_step_repeatable(rid, side, n, R):
 
 
 @pytest.mark.parametrize('F,act,dropout,cin,side,n', [(64, 'softsign', 0.2, 88, 88, 8), (64, 'tanh', 0.0, 96, 87, 5),
-                                                      (40, 'softsign', 0.3, 88, 64, 10), (64, 'softsign', 1e-4, 88, 88, 6)])
+                                                      (40, 'softsign', 0.3, 88, 64, 10), (64, 'softsign', 1e-4, 88, 88, 6),
+                                                      (64, 'softsign', 0.1, 88, 87, 5)])
 def test_train_step_rows_kernel(F, act, dropout, cin, side, n):
     """The row-parallel split training kernel for narrow hidden layers (csrc/hpe_mlp2.hip
     mlp2r_kernel: F <= 64, launches of >= 2^15 rows, train_88.py:66-140's 88 -> 64 softsign -> 3)
@@ -484,6 +485,32 @@ def test_train_step_rows_kernel(F, act, dropout, cin, side, n):
     go = grad(xot)
     assert np.isfinite(go).all()
     np.testing.assert_array_equal(go, go_exact)
+
+
+def test_rows_kernel_fit_matches_oracle():
+    """Model.fit on mlp2r_kernel (F = 64 softsign, dropout on both layers, 88x88 maps: 8 images =
+    61,952 rows per step) through fit's gathered batches (the image-index LDS-DMA path of the packed
+    88-float rows), 2 epochs of Adam against the oracle's fit with the same dropout masks."""
+    hpe.set_seed(5)
+    keras.backend.clear_session()
+    reg = keras.regularizers.l2(1e-6)
+    inp = keras.Input(shape=(None, None, 88))
+    h = keras.layers.Conv2D(64, 1, padding='same', activation='softsign', kernel_regularizer=reg)(inp)
+    h = keras.layers.SpatialDropout2D(0.1)(h)
+    o = keras.layers.Conv2D(3, 1, padding='same', kernel_regularizer=reg)(h)
+    o = keras.layers.SpatialDropout2D(0.1)(o)
+    m = keras.Model(inp, o)
+    m.compile(optimizer=keras.optimizers.Adam(learning_rate=2.8e-4), loss='mse', metrics=['mae'])
+    w0 = m.weights_dict()
+    n, side, bs = 12, 88, 8
+    x = features(n, 88, seed=9, h=side, w=side)
+    y = labels(n, seed=10)
+    hist = m.fit(x, y, batch_size=bs, epochs=2, shuffle=False, verbose=0)
+    g = _oracle_fit(m.model_config, w0, 'adam', x, y, bs, 2)
+    got = m.weights_dict()
+    for k in g.trainable:
+        np.testing.assert_allclose(got[k], g.params[k].detach().numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
+    assert np.isfinite(hist.history['loss']).all()
 
 
 def _create_model(F, act, dropout, l2, lr=2.8e-4):
