@@ -577,8 +577,9 @@ def bench_blazeface(dev, iters, no_cpu):
                         'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
                         'frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
                         'traffic': _traffic('blazeface'),
-                        'kernel': 'bf_stem_kernel + bf_* blocks + 2 head GEMMs + 2 regressor '
-                                  'programs (hpe_blazeface_forward + hpe_forward), whole forward',
+                        'kernel': 'bf_front_kernel (stem + 64x64 / 32x32 blocks) + bf_stage_kernel (16x16 / 8x8 '
+                                  'blocks + detector heads) + 2 pose regressor programs (hpe_blazeface_forward '
+                                  '+ hpe_forward), whole forward',
                         'kernel_ms': ms, 'bytes_per_launch': nbytes * BLAZE_B,
                         'plan_bytes': plan_bytes * BLAZE_B,
                         'plan_frac': plan_bytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
