@@ -488,8 +488,16 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       }
     }
     STAMP(4);
+    // PRE with >= 4 waves: the next tile's pre-split runs on waves 2.. during the head (waves 0-1),
+    // so its pieces must have landed by this barrier instead of the next one
+    const bool early = PRE && NCB >= 4;
+    if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar_lds();
     STAMP(5);
+    if constexpr (PRE) {
+      if (early && wave >= 2 && tile + gridDim.x < ntiles)
+        presplit_tile<KH>(xbuf, xfb, xtb + (buf ^ 1) * 3 * 96 * MLP2_TS, threadIdx.x - 128, NT - 128);
+    }
 
     // ---- head: sum partials (fixed wave order) + b2, epilogue, loss / output ----
     for (int it = threadIdx.x; it < T * 3 && threadIdx.x < NT3; it += NT3) {
@@ -544,13 +552,13 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     STAMP(6);
     if constexpr (PRE) {
       // the next tile landed -> barrier -> split it (forward layout: this tile's forward is done;
-      // transposed: the other parity, this tile's backward reads its own).  Splitting it earlier,
-      // by waves 2.. during the head (after a vmcnt(0) before the second barrier), measured slower
-      // (3.80 -> 3.92 ms, round 2 A/B)
+      // transposed: the other parity, this tile's backward reads its own), unless waves 2.. split
+      // it during the head above (`early`: round 2 measured that slower, 3.80 -> 3.92 ms; on the
+      // round-5 kernel it is faster, 3.235 -> 3.128 ms on configs[3], A/B x3)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar_lds();
       STAMP(7);
-      if (tile + gridDim.x < ntiles) {
+      if (!early && tile + gridDim.x < ntiles) {
         presplit_tile<KH>(xbuf, xfb, xtb + (buf ^ 1) * 3 * 96 * MLP2_TS, threadIdx.x, NT);
       }
       if (!train) continue;
