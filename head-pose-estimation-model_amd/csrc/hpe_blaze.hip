@@ -674,14 +674,18 @@ __global__ void __launch_bounds__(256) bf_direct_kernel(BfArgs a) {
 // one op of a stage (host-filled from its BFO record)
 struct BfSub {
   int s, h, w, ho, wo, cin, cinp, cout, coutp, ks, nct, nc, res, relu, dw, padt, padl, dww, pww, pwb;
-  int gsrc;     // 1: the source map is the stage input in global memory (first op), 0: the LDS map
+  int var;      // task variant (BFV_*), picked on the host
+  int wto;      // this op's W^T at wt + wto (the band op keeps it clear of its staging rows)
+  int sst;      // BFV_BAND: channel stride of the staged source rows
+  int ss, cso;  // channel strides of the resident source map (cinp + 4) and of the output map
+  int zhalo;    // 1: zero the output map's halo rows (its geometry differs from the source's)
   int lds_out;  // 1: the output map stays in LDS (blocks)
   int gdst, gdst2, split, ostride;  // global output buffer(s): taps (gdst), heads (split epilogue); -1 none
 };
 #define BFS_MAX 16
 struct BfStageArgs {
   BfSub op[BFS_MAX];
-  int nops, cs, map_floats, wt_floats;
+  int nops, map_floats, wt_floats;
   const float* params;
   const float* src;
   float* bufs[BF_NBUF];
@@ -702,9 +706,28 @@ struct BfStageArgs {
 //        split MFMA over ascending channel quads, bias, residual, ReLU), so the outputs are
 //        bit-identical to the per-op path; the next op's weights are loaded into registers while
 //        this op computes and written to LDS after its barrier (two barriers per op).
+//   round 6: NC is a template parameter of the task (a runtime NC made every MFMA triple
+//        conditional: an accumulator copy and an MFMA drain per K-step), the K loop keeps the next
+//        K-step's reads in flight while the current one computes, the first op (s2 from the
+//        32x32 map in HBM) stages its source through LDS in two row bands (BFV_BAND) instead of
+//        nine dependent global tap reads per K-step (22 % of the stage's cycles), and a tap map
+//        leaves LDS by a coalesced 16-B copy during the next op (was 4-B stores in the epilogue).
 // ------------------------------------------------------------------------------------------------
 #define BFS_NW 8
 #define BFS_PF 6     // float4 of the next op's W^T + dw table per thread (checked on the host)
+#define BFS_BQ 16    // float4 of a staged band per thread (checked on the host)
+#define BFV_GLOBAL 0  // first op, taps read from the map in global memory
+#define BFV_BAND 1    // first op, s2 on a 16-wide output: source rows staged in LDS, two bands
+#define BFV_DPP16 2   // s1 block on a 16-wide resident map (x-neighbour taps by DPP, no tap masks)
+#define BFV_DPP8 3    // s1 block on an 8-wide resident map (x-neighbour taps by DPP)
+#define BFV_S1 4      // s1 block on the resident map, nine tap reads
+#define BFV_MP 5      // s2 max-pool block on the resident map
+#define BFV_HEAD 6    // 1x1 detector head on the resident tap
+// resident maps carry a zero row above and below (the map's row 0 sits one row into the map
+// region, channel stride coutp + 4 of the op that wrote it): taps on rows -1 / H read zeros, the
+// value the tap mask would give (bit-identical), so those taps need no mask
+
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ void bfs_wload(const BfSub& o, const float* P_, f32x4 (&pf)[BFS_PF]) {
   const int kq = o.cinp >> 2, nW = o.coutp * kq, nT = nW + (o.dw ? 10 * kq : 0);
@@ -719,6 +742,7 @@ __device__ __forceinline__ void bfs_wload(const BfSub& o, const float* P_, f32x4
 
 __device__ __forceinline__ void bfs_wstore(const BfSub& o, const f32x4 (&pf)[BFS_PF], float* wt, float* dwt) {
   const int kq = o.cinp >> 2, nW = o.coutp * kq, nT = nW + (o.dw ? 10 * kq : 0);
+  wt += o.wto;
 #pragma unroll
   for (int i = 0; i < BFS_PF; ++i) {
     const int e = threadIdx.x + i * (BFS_NW * 64);
@@ -728,10 +752,6 @@ __device__ __forceinline__ void bfs_wstore(const BfSub& o, const f32x4 (&pf)[BFS
   }
 }
 
-// one wave task of op o: acc[j] (j < o.nc) = the final outputs (bias, residual, ReLU applied) of
-// output-channel chunk grp * nc + j at the 32 positions of chunk `chunk`; src = the input map
-// (global: the stage input of this image, channel stride cinp; LDS: the resident map, stride cs)
-#define BFS_MAXNC 3  // output-channel chunks per wave task (acc registers: 16 each)
 // DPP (stride-1 depthwise ops on 16- or 8-wide maps from the LDS map): per 3x3 row one ds_read_b128
 // of the centre column, the x-neighbours by DPP row shifts of it (a 16-lane DPP row is one 16-wide
 // map row or two 8-wide ones; lanes whose neighbour is across a map-row edge are zeroed by the tap
@@ -742,42 +762,122 @@ __device__ __forceinline__ float dpp_from_prev(float v) {  // lane i <- lane i -
 __device__ __forceinline__ float dpp_from_next(float v) {  // lane i <- lane i + 1 of its 16-lane row
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));
 }
-template <bool G, bool DW, int RES, bool DPP = false>
-__device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int ss, const float* wt,
+
+#define BFS_MAXNC 3  // output-channel chunks per wave task (acc registers: 16 each)
+#ifndef BFS_PIPE
+#define BFS_PIPE 0   // 1: the K loop prefetches the next step's taps / W^T (more VGPRs: spills)
+#endif
+#ifdef BFS_SB_ON   // a scheduling barrier after each step's reads (measured slower: more spills)
+#define BFS_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define BFS_SB() do {} while (0)
+#endif
+// the streamed maps (the stage's source rows, taps and head outputs, each touched once) bypass
+// L2 retention (non-temporal), so the stage's weights, re-read by every frame, stay L2-resident
+#ifndef BFS_NT
+#define BFS_NT 1
+#endif
+__device__ __forceinline__ f32x4 ld4_nt(const float* p) {
+  if (BFS_NT) return __builtin_nontemporal_load((const f32x4*)p);
+  return *(const f32x4*)p;
+}
+__device__ __forceinline__ void st4_nt(float* p, f32x4 v) {
+  if (BFS_NT) __builtin_nontemporal_store(v, (f32x4*)p);
+  else *(f32x4*)p = v;
+}
+__device__ __forceinline__ void st1_nt(float* p, float v) {
+  if (BFS_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// the prefetched reads of one K-step (8 input channels; this lane's quad c0 = 4 half + 8 k); the
+// depthwise table rows (10 broadcast quads) are read inside the step, ahead of the taps' DPP work
+template <int NT, int NC>
+struct BfsK {
+  f32x4 x[NT];                  // source taps (DPP: the 3 centre-column reads)
+  f32x4 w[NC];                  // W^T quads (fp16 hi/lo pairs) of the NC output-channel chunks
+};
+
+// one wave task of op o: acc[j] (j < NC) = the final outputs (bias, residual, ReLU applied) of
+// output-channel chunk grp * NC + j at the 32 positions of chunk `chunk`.  src: the source map
+// (global: the stage input of this image; LDS: the resident map or, BFV_BAND, the staged rows
+// iyb.. of the source), channel stride ss.
+template <int V, int RES, int NC>
+__device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int ss, int iyb, const float* wt,
                                          const float* dwt, const float* P_, int chunk, int grp,
                                          f32x16 (&acc)[BFS_MAXNC]) {
+  constexpr bool DW = V != BFV_HEAD, DPP = V == BFV_DPP16 || V == BFV_DPP8;
+  constexpr int NT = !DW ? 1 : (DPP ? 3 : 9), ND = DW ? 10 : 0;
+  // taps that need the mask: rows -1 / H of a resident map are its zero halo rows; a 16-wide
+  // map's x-neighbours come from DPP row shifts, zero at the row ends (bound_ctrl)
+  constexpr bool YH = V == BFV_DPP16 || V == BFV_DPP8 || V == BFV_S1 || V == BFV_MP;
+  auto masked = [](int tp) constexpr {
+    const int dy = tp / 3, dx = tp % 3;
+    if (V == BFV_DPP16) return false;
+    if (V == BFV_MP) return dx == 2;
+    if (YH) return dx != 1;
+    (void)dy;
+    return true;
+  };
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  // the op's fields as wave-uniform registers for the whole task (read from the kernel arguments
-  // once: left as references the compiler re-loads them from kernarg inside the K loop, and every
-  // s_load there serialises the LDS reads behind an lgkmcnt(0))
-  const int cinp = __builtin_amdgcn_readfirstlane(o.cinp), ks = __builtin_amdgcn_readfirstlane(o.ks);
-  const int coutp = __builtin_amdgcn_readfirstlane(o.coutp), nc = __builtin_amdgcn_readfirstlane(o.nc);
-  const int ow = __builtin_amdgcn_readfirstlane(o.w), wo = __builtin_amdgcn_readfirstlane(o.wo);
+  // the op's fields as wave-uniform registers (left as references the compiler re-loads them
+  // from kernarg inside the K loop, each s_load behind an lgkmcnt(0))
+  const int cinp = rfl(o.cinp), ks = rfl(o.ks), coutp = rfl(o.coutp);
+  const int ow = rfl(o.w), wo = rfl(o.wo), oh = rfl(o.h), S = rfl(o.s), padt = rfl(o.padt), padl = rfl(o.padl);
   const int lgWo = __builtin_ctz(wo);
   const int p = chunk * 32 + l32;
   const int oy = p >> lgWo, ox = p & (wo - 1);
   int toff[9];
   uint32_t tmask = 0;
+  {
+    // masked taps read the centre tap's (always valid) offset: no read outside the staged rows
+    const int cy = oy * S - padt + 1, cx = ox * S - padl + 1;
+    const bool cok = cy >= 0 && cy < oh && cx >= 0 && cx < ow;
+    const int cen = cok ? ((cy - iyb) * ow + cx) * ss : 0;
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp) {
-    const int iy = oy * o.s - o.padt + tp / 3, ix = ox * o.s - o.padl + tp % 3;
-    const bool ok = iy >= 0 && iy < o.h && ix >= 0 && ix < ow;
-    toff[tp] = ok ? (iy * ow + ix) * ss : 0;
-    tmask |= ok ? (1u << tp) : 0u;
+    for (int tp = 0; tp < 9; ++tp) {
+      const int iy = oy * S - padt + tp / 3, ix = ox * S - padl + tp % 3;
+      const bool ok = iy >= 0 && iy < oh && ix >= 0 && ix < ow;
+      // an unmasked tap's row may be a halo row (x always in range for those)
+      toff[tp] = ok || !masked(tp) ? ((iy - iyb) * ow + ix) * ss : cen;
+      tmask |= ok ? (1u << tp) : 0u;
+    }
+    if (!DW) toff[0] = ((oy - iyb) * ow + ox) * ss;
   }
-  const int cen = (oy * ow + ox) * ss;
+  const int n0 = grp * NC * 32 + l32;
+  float bias[NC];
+  int wrow[NC];
 #pragma unroll
-  for (int j = 0; j < BFS_MAXNC; ++j) acc[j] = (f32x16){};
-  const int n0 = grp * nc * 32 + l32;
-#pragma unroll 2
-  for (int c0 = 4 * half; c0 < cinp; c0 += 8) {
+  for (int j = 0; j < NC; ++j) {
+    const int n = n0 + 32 * j;
+    bias[j] = n < coutp ? P_[o.pwb + n] : 0.f;
+    wrow[j] = (n < coutp ? n : coutp - 1) * ks;  // columns past coutp: finite weights, outputs unused
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j] = (f32x16){};
+
+  using K = BfsK<NT, NC>;
+  typedef f32x4 Dv[ND > 0 ? ND : 1];
+  auto load = [&](int c0, K& r) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) r.x[t] = ld4(src + toff[DPP ? 3 * t + 1 : t] + c0);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) r.w[j] = ld4(wt + wrow[j] + c0);
+  };
+  // the step's depthwise table rows, issued as one batch ahead of the prefetch of the next step
+  // (left to the scheduler, each row was read behind its own lgkmcnt(0): an LDS round trip per row)
+  auto load_dw = [&](int c0, Dv& dv) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) dv[t] = ld4(dwt + t * cinp + c0);
+  };
+  auto step = [&](const K& r, const Dv& dv) {
     f32x4 av;
-    if (DW) {
+    if constexpr (DW) {
       f32x4 xv[9];
-      if (DPP) {
+      if constexpr (DPP) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy) {
-          const f32x4 c = ld4(src + toff[3 * dy + 1] + c0);
+          const f32x4 c = r.x[dy];
           xv[3 * dy + 1] = c;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -787,52 +887,172 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
         }
       } else {
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) xv[tp] = ld4(src + toff[tp] + c0);
+        for (int tp = 0; tp < 9; ++tp) xv[tp] = r.x[tp];
       }
-      av = ld4(dwt + 9 * cinp + c0);
+      av = dv[9];
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp) {
-        const f32x4 x = (tmask >> tp) & 1u ? xv[tp] : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 wv = ld4(dwt + tp * cinp + c0);
+        const f32x4 x = !masked(tp) || ((tmask >> tp) & 1u) ? xv[tp] : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 wv = dv[tp];
         av.x = fmaf(x.x, wv.x, av.x);
         av.y = fmaf(x.y, wv.y, av.y);
         av.z = fmaf(x.z, wv.z, av.z);
         av.w = fmaf(x.w, wv.w, av.w);
       }
     } else {
-      av = ld4(src + cen + c0);
+      av = r.x[0];
     }
 #pragma unroll
-    for (int j = 0; j < BFS_MAXNC; ++j) {
-      if (j < nc) {
-        const int n = n0 + 32 * j;
-        const f32x4 wv = n < coutp ? ld4(wt + n * ks + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
-        acc[j] = mfma_split(av, wv, acc[j]);
-      }
+    for (int j = 0; j < NC; ++j) acc[j] = mfma_split(av, r.w[j], acc[j]);
+  };
+  // K loop, two steps per trip: the next step's reads are issued before this step's arithmetic
+  // (BFV_BAND: one buffer, its registers hold the second band's staged rows meanwhile; BFV_GLOBAL
+  // too, the generic fallback)
+  const int nks = cinp >> 3;
+  int c0 = 4 * half;
+  Dv dv;
+  if constexpr (V == BFV_BAND || V == BFV_GLOBAL || !BFS_PIPE) {
+    for (int k = 0; k < nks; ++k, c0 += 8) {
+      K A;
+      load_dw(c0, dv);
+      load(c0, A);
+      if constexpr (V != BFV_BAND && V != BFV_GLOBAL) BFS_SB();
+      step(A, dv);
+    }
+  } else {
+    K A, B;
+    load(c0, A);
+    int k = 0;
+    for (; k + 2 <= nks; k += 2, c0 += 16) {
+      load_dw(c0, dv);
+      load(c0 + 8, B);
+      BFS_SB();
+      step(A, dv);
+      load_dw(c0 + 8, dv);
+      load(k + 2 < nks ? c0 + 16 : c0 + 8, A);
+      BFS_SB();
+      step(B, dv);
+    }
+    if (nks & 1) {
+      load_dw(c0, dv);
+      BFS_SB();
+      step(A, dv);
     }
   }
+
   // epilogue values: lane = output channel n, registers = 16 positions of the chunk
 #pragma unroll
-  for (int j = 0; j < BFS_MAXNC; ++j) {
-    if (j >= nc) continue;
+  for (int j = 0; j < NC; ++j) {
     const int n = n0 + 32 * j;
-    const float bias = n < coutp ? P_[o.pwb + n] : 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
       const int qy = q >> lgWo, qx = q & (wo - 1);
-      float v = acc[j][g] + bias;
+      float v = acc[j][g] + bias[j];
       if (RES == BF_RES_ID) {
-        if (n < cinp) v += src[(qy * ow + qx) * ss + n];
+        if (n < cinp) v += src[((qy - iyb) * ow + qx) * ss + n];
       } else if (RES == BF_RES_MAXPOOL) {
         if (n < cinp) {
-          const float* t = src + ((2 * qy) * ow + 2 * qx) * ss + n;
+          const float* t = src + ((2 * qy - iyb) * ow + 2 * qx) * ss + n;
           v += fmaxf(fmaxf(t[0], t[ss]), fmaxf(t[ow * ss], t[ow * ss + ss]));
         }
       }
-      if (DW && o.relu) v = v > 0.f ? v : 0.f;
+      if (DW) v = v > 0.f ? v : 0.f;
       acc[j][g] = v;
     }
+  }
+}
+
+// the task of op o for this wave (variant and NC dispatched to the compile-time instantiations)
+__device__ __forceinline__ void bfs_dispatch(const BfSub& o, int var, int nc, const float* src, int ss, int iyb,
+                                             const float* wt, const float* dwt, const float* P_, int chunk,
+                                             int grp, f32x16 (&acc)[BFS_MAXNC]) {
+  const int res = rfl(o.res);
+#define BFS_NCS(V_, R_)                                                              \
+  switch (nc) {                                                                      \
+    case 1: bfs_task<V_, R_, 1>(o, src, ss, iyb, wt, dwt, P_, chunk, grp, acc); break; \
+    case 2: bfs_task<V_, R_, 2>(o, src, ss, iyb, wt, dwt, P_, chunk, grp, acc); break; \
+    default: bfs_task<V_, R_, 3>(o, src, ss, iyb, wt, dwt, P_, chunk, grp, acc); break; \
+  }
+  switch (var) {
+    case BFV_GLOBAL:
+      if (res == BF_RES_MAXPOOL) { BFS_NCS(BFV_GLOBAL, BF_RES_MAXPOOL) } else { BFS_NCS(BFV_GLOBAL, BF_RES_ID) }
+      break;
+    case BFV_BAND: bfs_task<BFV_BAND, BF_RES_MAXPOOL, 1>(o, src, ss, iyb, wt, dwt, P_, chunk, grp, acc); break;
+    case BFV_DPP16: BFS_NCS(BFV_DPP16, BF_RES_ID) break;
+    case BFV_DPP8: BFS_NCS(BFV_DPP8, BF_RES_ID) break;
+    case BFV_S1: BFS_NCS(BFV_S1, BF_RES_ID) break;
+    case BFV_MP: BFS_NCS(BFV_MP, BF_RES_MAXPOOL) break;
+    default: BFS_NCS(BFV_HEAD, BF_RES_NONE) break;
+  }
+#undef BFS_NCS
+}
+
+// BFV_BAND staging: rows [r0, r1) of the source map (contiguous in global memory) into LDS at
+// channel stride sst; registers first (the second band's loads fly during the first band's work)
+__device__ __forceinline__ void bfs_band_load(const float* g, int nq, f32x4 (&r)[BFS_BQ]) {
+#pragma unroll
+  for (int i = 0; i < BFS_BQ; ++i) {
+    const int e = threadIdx.x + i * (BFS_NW * 64);
+    r[i] = ld4_nt(g + 4 * (e < nq ? e : nq - 1));
+  }
+}
+__device__ __forceinline__ void bfs_band_store(float* st, int nq, int kq, int sst, const f32x4 (&r)[BFS_BQ]) {
+  const float inv = 1.f / (float)kq;
+#pragma unroll
+  for (int i = 0; i < BFS_BQ; ++i) {
+    const int e = threadIdx.x + i * (BFS_NW * 64);
+    if (e < nq) {
+      const int pix = (int)(((float)e + 0.5f) * inv), q = e - pix * kq;  // exact for e < 2^16
+      *(f32x4*)(st + pix * sst + 4 * q) = r[i];
+    }
+  }
+}
+
+// the epilogue stores of one wave task: the map (blocks) and / or the head outputs in HBM
+__device__ __forceinline__ void bfs_store(const BfSub& o, const float* const* bufs, float* map, int cs, int64_t img,
+                                          int chunk, int grp, const f32x16 (&acc)[BFS_MAXNC]) {  // map: row 0
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int64_t hwo = o.ho * o.wo;
+  const bool head = !o.dw;
+  float* gd = head ? (float*)bufs[o.gdst] : nullptr;
+  float* gd2 = head && o.split ? (float*)bufs[o.gdst2] : nullptr;
+  const int nc = rfl(o.nc), coutp = rfl(o.coutp);
+  const int split = rfl(o.split), cout = rfl(o.cout), ostride = rfl(o.ostride);
+#pragma unroll
+  for (int j = 0; j < BFS_MAXNC; ++j) {
+    if (j >= nc) continue;
+    const int n = (grp * nc + j) * 32 + l32;
+    if (n >= coutp) continue;
+    if (!head) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) map[(chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * cs + n] = acc[j][g];
+      continue;
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
+      const float v = acc[j][g];
+      const int64_t pos = img * hwo + q;
+      if (split) {
+        if (n < split) st1_nt(gd + pos * split + n, v);
+        else if (n < cout) st1_nt(gd2 + pos * (cout - split) + (n - split), v);
+      } else if (n < ostride) {
+        st1_nt(gd + pos * ostride + n, v);
+      }
+    }
+  }
+}
+
+// a tap map (the resident map after op o) to its caller buffer: [img][HW][coutp], 16-B pieces
+__device__ __forceinline__ void bfs_tap_copy(const BfSub& o, const float* const* bufs, const float* lmap, int64_t img) {
+  const int kq = rfl(o.coutp) >> 2, hw = rfl(o.ho * o.wo), nq = hw * kq, cs = rfl(o.cso);
+  const float* map = lmap + rfl(o.wo) * cs;  // row 0
+  float* gd = (float*)bufs[o.gdst] + img * hw * (kq * 4);
+  const float inv = 1.f / (float)kq;
+  for (int e = threadIdx.x; e < nq; e += BFS_NW * 64) {
+    const int pix = (int)(((float)e + 0.5f) * inv), q = e - pix * kq;
+    st4_nt(gd + 4 * e, ld4(map + pix * cs + 4 * q));
   }
 }
 
@@ -842,73 +1062,94 @@ __global__ void __launch_bounds__(BFS_NW * 64) bf_stage_kernel(BfStageArgs a) {
   float* wt = lds + a.map_floats;
   float* dwt = wt + a.wt_floats;
   const int64_t img = blockIdx.x;
-  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float* P_ = a.params;
-  const int cs = a.cs;
   f32x4 pf[BFS_PF];
   bfs_wload(a.op[0], P_, pf);
   bfs_wstore(a.op[0], pf, wt, dwt);
   __syncthreads();
+#ifdef BFS_STAMPS   // per-op, per-wave cycles of workgroup 0: compute | barrier 1 | stores | barrier 2
+  uint32_t bst[BFS_MAX][4];
+  uint64_t bt = __builtin_amdgcn_s_memtime();
+#define BFS_ST(i, k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); bst[i][k] = (uint32_t)(t_ - bt); bt = t_; } while (0)
+#else
+#define BFS_ST(i, k) do {} while (0)
+#endif
+  int tap = -1;  // op whose output map is a tap still to be copied out of LDS
   for (int i = 0; i < a.nops; ++i) {
     const BfSub& o = a.op[i];
     if (i + 1 < a.nops) bfs_wload(a.op[i + 1], P_, pf);
-    const int ngrp = o.nct / o.nc;
-    const int ntask = ((o.ho * o.wo) >> 5) * ngrp;
-    const int chunk = wave / ngrp, grp = wave - chunk * ngrp;
-    f32x16 acc[BFS_MAXNC];
-    if (wave < ntask) {
-      const float* gs = a.src + img * o.h * o.w * o.cinp;
-      if (o.gsrc) {
-        if (o.res == BF_RES_MAXPOOL) bfs_task<true, true, BF_RES_MAXPOOL>(o, gs, o.cinp, wt, dwt, P_, chunk, grp, acc);
-        else bfs_task<true, true, BF_RES_ID>(o, gs, o.cinp, wt, dwt, P_, chunk, grp, acc);
-      } else if (!o.dw) {
-        bfs_task<false, false, BF_RES_NONE>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
-      } else if (o.res == BF_RES_MAXPOOL) {
-        bfs_task<false, true, BF_RES_MAXPOOL>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
-      } else if (o.s == 1 && o.res == BF_RES_ID && (o.wo == 16 || o.wo == 8) && o.w == o.wo && o.padl == 1) {
-        bfs_task<false, true, BF_RES_ID, true>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+    if (tap >= 0) bfs_tap_copy(a.op[tap], a.bufs, map, img);  // the map is rewritten after barrier 1
+    tap = -1;
+    const int var = rfl(o.var), nc = rfl(o.nc);
+    const int ngrp = rfl(o.nct) / nc;
+    const float* wto = wt + rfl(o.wto);
+    f32x16 acc[BFS_MAXNC], acc2[BFS_MAXNC];
+    int chunk, chunk2 = -1, grp;
+    if (var == BFV_BAND) {
+      // two bands of output rows, each 4 chunks x ngrp tasks; the source rows of band b:
+      // [b H / 2, b H / 2 + H / 2 + 1) clipped to the map, staged at LDS offset 0 (stride sst)
+      const int H = rfl(o.h), W = rfl(o.w), kq = rfl(o.cinp) >> 2, sst = rfl(o.sst);
+      const float* gsrc = a.src + img * H * W * (kq * 4);
+      const int hb = H >> 1;
+      const int nq0 = (hb + 1) * W * kq, nq1 = (H - hb) * W * kq;
+      f32x4 r[BFS_BQ];
+      bfs_band_load(gsrc, nq0, r);
+      bfs_band_store(lds, nq0, kq, sst, r);
+      bfs_band_load(gsrc + hb * W * kq * 4, nq1, r);  // in flight over band 0
+      __syncthreads();
+      const bool busy = wave < 4 * ngrp;
+      chunk = busy ? wave / ngrp : -1;
+      grp = wave - (wave / ngrp) * ngrp;
+      if (busy) bfs_dispatch(o, var, nc, lds, sst, 0, wto, dwt, P_, chunk, grp, acc);
+      __syncthreads();
+      bfs_band_store(lds, nq1, kq, sst, r);
+      __syncthreads();
+      chunk2 = busy ? chunk + 4 : -1;
+      if (busy) bfs_dispatch(o, var, nc, lds, sst, hb, wto, dwt, P_, chunk2, grp, acc2);
+    } else {
+      const int ntask = ((rfl(o.ho) * rfl(o.wo)) >> 5) * ngrp;
+      chunk = wave / ngrp;
+      grp = wave - chunk * ngrp;
+      if (wave < ntask) {
+        if (var == BFV_GLOBAL) {
+          const float* gs = a.src + img * o.h * o.w * o.cinp;
+          bfs_dispatch(o, var, nc, gs, rfl(o.cinp), 0, wto, dwt, P_, chunk, grp, acc);
+        } else {
+          const int ss = rfl(o.ss);
+          bfs_dispatch(o, var, nc, map + rfl(o.w) * ss, ss, 0, wto, dwt, P_, chunk, grp, acc);
+        }
       } else {
-        bfs_task<false, true, BF_RES_ID>(o, map, cs, wt, dwt, P_, chunk, grp, acc);
+        chunk = -1;
       }
     }
+    BFS_ST(i, 0);
     __syncthreads();  // every wave's reads of the map and of W^T are done
-    if (wave < ntask) {
-      const int64_t hwo = o.ho * o.wo;
-      float* gd = o.gdst >= 0 ? a.bufs[o.gdst] : nullptr;
-      float* gd2 = o.split ? a.bufs[o.gdst2] : nullptr;
-      const int nc = __builtin_amdgcn_readfirstlane(o.nc), coutp = __builtin_amdgcn_readfirstlane(o.coutp);
-      const int split = __builtin_amdgcn_readfirstlane(o.split), cout = __builtin_amdgcn_readfirstlane(o.cout);
-      const int ostride = __builtin_amdgcn_readfirstlane(o.ostride), lds_out = __builtin_amdgcn_readfirstlane(o.lds_out);
-#pragma unroll
-      for (int j = 0; j < BFS_MAXNC; ++j) {
-        if (j >= nc) continue;
-        const int n = (grp * nc + j) * 32 + l32;
-        if (n >= coutp) continue;
-        if (lds_out) {
-#pragma unroll
-          for (int g = 0; g < 16; ++g) map[(chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half) * cs + n] = acc[j][g];
-        }
-        if (!gd) continue;
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
-          const float v = acc[j][g];
-          {
-            const int64_t pos = img * hwo + q;
-            if (split) {
-              if (n < split) gd[pos * split + n] = v;
-              else if (n < cout) gd2[pos * (cout - split) + (n - split)] = v;
-            } else if (n < ostride) {
-              gd[pos * ostride + n] = v;
-            }
-          }
-        }
+    BFS_ST(i, 1);
+    {
+      const int cso = rfl(o.cso), wo = rfl(o.wo);
+      float* orow = map + wo * cso;
+      if (chunk >= 0) bfs_store(o, a.bufs, orow, cso, img, chunk, grp, acc);
+      if (chunk2 >= 0) bfs_store(o, a.bufs, orow, cso, img, chunk2, grp, acc2);
+      if (o.zhalo) {  // rows -1 and HO of the new map
+        const int rq = wo * cso / 4, ho = rfl(o.ho);
+        for (int e = threadIdx.x; e < 2 * rq; e += BFS_NW * 64)
+          *(f32x4*)(map + (e < rq ? 4 * e : (ho + 1) * wo * cso + 4 * (e - rq))) = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+    if (o.dw && o.gdst >= 0) tap = i;
     if (i + 1 < a.nops) bfs_wstore(a.op[i + 1], pf, wt, dwt);
+    BFS_ST(i, 2);
     __syncthreads();  // outputs and the next op's weights visible
+    BFS_ST(i, 3);
   }
+  if (tap >= 0) bfs_tap_copy(a.op[tap], a.bufs, map, img);
+#ifdef BFS_STAMPS
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+    for (int i = 0; i < a.nops; ++i)
+      printf("BFS op %d w %d comp %u bar1 %u store %u bar2 %u\n", i, wave, bst[i][0], bst[i][1], bst[i][2], bst[i][3]);
+#endif
+#undef BFS_ST
 }
 
 typedef void (*bf_fn)(BfArgs);
@@ -1328,6 +1569,42 @@ static int bfs_nc(int nchunk, int nct) {
     if (nct % nc == 0 && nchunk * (nct / nc) <= BFS_NW) return nc;
   return 0;
 }
+// the NC a stage op runs with: BFS_NCMAX prefers the most output-channel chunks per task (fewer
+// tasks, the depthwise work done once per position chunk) over the most busy waves
+static int bfs_nc_run(int nchunk, int nct) {
+#ifdef BFS_NCMAX
+  for (int nc = nct < BFS_MAXNC ? nct : BFS_MAXNC; nc >= 1; --nc)
+    if (nct % nc == 0 && nchunk * (nct / nc) <= BFS_NW) return nc;
+#endif
+  return bfs_nc(nchunk, nct);
+}
+
+// the task variant of stage op k (record g); the band op (the first op, s2 onto a 16x16 map) also
+// gets its W^T placed at the end of the W^T region (wto), clear of its staged source rows, which
+// start at LDS offset 0 (stride sst), and its own NC (4 chunks per band)
+static int bfs_variant(const int* g, int k, int mapf, int wtf, int* wto, int* sst, int* nc) {
+  const int s = g[BFO_STRIDE], dw = g[BFO_DW], res = g[BFO_RES], wo = g[BFO_WO], ho = g[BFO_HO];
+  *wto = 0;
+  *sst = 0;
+  if (k == 0) {
+    const int H = g[BFO_H], W = g[BFO_W], cinp = g[BFO_CINP], kq = cinp / 4;
+    const int band_nc = bfs_nc(4, g[BFO_NCT]);  // the band task is compiled for NC = 1
+    const int wt_at = wtf - g[BFO_COUTP] * g[BFO_KS];
+    if (dw && s == 2 && res == BF_RES_MAXPOOL && !g[BFO_PADT] && !g[BFO_PADL] && ho == 16 && wo == 16 &&
+        H == 2 * ho && W == 2 * wo && band_nc == 1 && (H / 2 + 1) * W * kq <= BFS_BQ * BFS_NW * 64 &&
+        (H / 2 + 1) * W * (cinp + 4) <= mapf + wt_at) {
+      *wto = wt_at;
+      *sst = cinp + 4;
+      *nc = band_nc;
+      return BFV_BAND;
+    }
+    return BFV_GLOBAL;
+  }
+  if (!dw) return BFV_HEAD;
+  if (res == BF_RES_MAXPOOL) return BFV_MP;
+  if (s == 1 && (wo == 16 || wo == 8) && g[BFO_W] == wo && g[BFO_PADL] == 1) return wo == 16 ? BFV_DPP16 : BFV_DPP8;
+  return BFV_S1;
+}
 
 static int check_stage(const int* f, int i, int rest) {
   const int ni = f[BFO_NI], cs = f[BFO_CS], mapf = f[BFO_ROWS], wtf = f[BFO_COLS], lds = f[BFO_LDS];
@@ -1354,11 +1631,11 @@ static int check_stage(const int* f, int i, int rest) {
     if (k == 0) {
       if (!dw || g[BFO_SRC] == BF_BUF_IMG) return hpe_fail(HPE_EINVAL, "blazeface stage %d: must start with a block reading a map", i);
     } else {
-      if (g[BFO_SRC] != last_dst || h * w * cs > mapf || cinp > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: source is not the resident map", i, k);
+      if (g[BFO_SRC] != last_dst || (h + 2) * w * (cinp + 4) > mapf || cinp + 4 > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: source is not the resident map", i, k);
       if (!dw && last_dst < BF_BUF_OUT0) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: heads must read a tap", i, k);
     }
     if (dw) {
-      if (ho * wo * cs > mapf || coutp > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: output map exceeds LDS", i, k);
+      if ((ho + 2) * wo * (coutp + 4) > mapf || coutp + 4 > cs) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: output map exceeds LDS", i, k);
       if (g[BFO_SPLIT] || g[BFO_OSTRIDE] != coutp) return hpe_fail(HPE_EINVAL, "blazeface stage %d op %d: block output stride", i, k);
       last_dst = g[BFO_DST];
     } else if (g[BFO_RES] != BF_RES_NONE || g[BFO_DST] < BF_BUF_OUT0) {
@@ -1563,7 +1840,6 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
       memset(&sa, 0, sizeof sa);
       const int ni = f[BFO_NI];
       sa.nops = ni;
-      sa.cs = f[BFO_CS];
       sa.map_floats = f[BFO_ROWS];
       sa.wt_floats = f[BFO_COLS];
       sa.params = params;
@@ -1573,10 +1849,15 @@ extern "C" int hpe_blazeface_forward(const hpe_blazeface* h, const float* params
         BfSub& o = sa.op[k];
         o.s = g[BFO_STRIDE]; o.h = g[BFO_H]; o.w = g[BFO_W]; o.ho = g[BFO_HO]; o.wo = g[BFO_WO];
         o.cin = g[BFO_CIN]; o.cinp = g[BFO_CINP]; o.cout = g[BFO_COUT]; o.coutp = g[BFO_COUTP];
-        o.ks = g[BFO_KS]; o.nct = g[BFO_NCT]; o.nc = bfs_nc((o.ho * o.wo) >> 5, o.nct);
+        o.ks = g[BFO_KS]; o.nct = g[BFO_NCT]; o.nc = bfs_nc_run((o.ho * o.wo) >> 5, o.nct);
         o.res = g[BFO_RES]; o.relu = g[BFO_RELU]; o.dw = g[BFO_DW]; o.padt = g[BFO_PADT]; o.padl = g[BFO_PADL];
         o.dww = g[BFO_DWW]; o.pww = g[BFO_PWW]; o.pwb = g[BFO_PWB];
-        o.gsrc = k == 0;
+        o.var = bfs_variant(g, k, sa.map_floats, sa.wt_floats, &o.wto, &o.sst, &o.nc);
+        o.ss = o.cinp + 4;
+        o.cso = o.coutp + 4;
+        // the first op's map replaces the staged rows / the source in global memory; a block whose
+        // output map differs in shape or stride from its source gets fresh halo rows
+        o.zhalo = g[BFO_DW] && (k == 0 || o.ho != o.h || o.wo != o.w || o.cso != o.ss);
         if (k == 0) sa.src = bufs[g[BFO_SRC]];
         o.lds_out = g[BFO_DW] ? 1 : 0;
         o.gdst = g[BFO_DW] ? (g[BFO_DST] >= BF_BUF_OUT0 ? g[BFO_DST] : -1) : g[BFO_DST];

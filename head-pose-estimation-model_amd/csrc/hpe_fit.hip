@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(FIT_NW * 64) fit_kernel(FitArgs a) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int r = r0 + (g & 3) + 8 * (g >> 2) + 4 * half;
-        float z = act1_f<ACT1>(act1, SPLIT ? fmaf(acc[g], inv1, b1n) : acc[g] + b1n);
+        float z = act1_f<ACT1, SPLIT>(act1, SPLIT ? fmaf(acc[g], inv1, b1n) : acc[g] + b1n);
         if (drop1 >= 0) {
           const bool kp = drop_hash(seed, drop1, (uint64_t)r, n) >= thr1;
           km |= kp ? (1u << g) : 0u;

@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
       const f32x4 cs = *(const f32x4*)(colt + n * 4);  // (inv1, b1, s2, -)
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        float z = act1_f<ACT1>(e1.act, SPLIT ? fmaf(acc[g], cs.x, cs.y) : acc[g] + cs.y);
+        float z = act1_f<ACT1, SPLIT>(e1.act, SPLIT ? fmaf(acc[g], cs.x, cs.y) : acc[g] + cs.y);
         if (DROP) z = (dmask >> g) & 1u ? z * inv_keep1 : 0.f;
         acc[g] = nok ? z : 0.f;
       }

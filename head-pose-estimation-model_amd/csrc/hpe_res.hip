@@ -98,12 +98,13 @@ struct RowMap {
   __device__ __forceinline__ uint64_t dimg(int64_t R) const { return fit ? (uint64_t)R : (uint64_t)(R / P + img_off); }
 };
 
-// the layer activations on the hot path: softsign / tanh in a few VALU ops (reciprocal and exp
-// approximations, ~1-2 ulp), the rest as the interpreter computes them (act_f)
+// the layer activations on the hot path: softsign in a few VALU ops (reciprocal approximation,
+// ~1 ulp relative), tanh as tanhf (these kernels are exact-fp32: hpe_dev.h fast_tanh5's absolute
+// error bound is for the fp16-split kernels only), the rest as the interpreter computes them
 __device__ __forceinline__ float res_act(int act, float z) {
   if (act == ACT_LINEAR) return z;
   if (act == ACT_SOFTSIGN) return z * __builtin_amdgcn_rcpf(1.f + fabsf(z));
-  if (act == ACT_TANH) return fast_tanh5(z);
+  if (act == ACT_TANH) return tanhf(z);
   if (act == ACT_RELU) return z > 0.f ? z : 0.f;
   return act_f(act, z);
 }

@@ -34,6 +34,7 @@
 #include "../../include/hpe.h"
 
 #include "hpe_common.h"
+#include "hpe_dev.h"
 
 
 
@@ -1073,6 +1074,33 @@ extern "C" int hpe_kernel_times(float* ms, int32_t max) {
     HIPCHK(hipEventElapsedTime(&ms[i], g_tev[2 * i], g_tev[2 * i + 1]));
   }
   return n;
+}
+
+// hpe_act_probe: the fused kernels' layer-1 activation (hpe_dev.h act1_f) on a buffer, for the
+// error bounds of tests/test_gpu_activations.py
+template <int ACT1, bool FAST>
+__global__ void act_probe_kernel(int act, const float* z, float* out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = act1_f<ACT1, FAST>(act, z[i]);
+}
+
+extern "C" int hpe_act_probe(int32_t act, int32_t fast, const float* z, float* out, int64_t n, void* stream) {
+  if (!z || !out || n < 0) return hpe_fail(HPE_EINVAL, "act_probe: bad argument");
+  if (act < ACT_LINEAR || act > ACT_LEAKY_RELU) return hpe_fail(HPE_EINVAL, "act_probe: activation %d", act);
+  if (n == 0) return HPE_OK;
+  const int64_t want = (n + 255) / 256;
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  hipStream_t s = (hipStream_t)stream;
+  if (act == ACT_TANH) {
+    if (fast) hipLaunchKernelGGL((act_probe_kernel<ACT_TANH, true>), dim3(grid), dim3(256), 0, s, act, z, out, n);
+    else hipLaunchKernelGGL((act_probe_kernel<ACT_TANH, false>), dim3(grid), dim3(256), 0, s, act, z, out, n);
+  } else if (act == ACT_SOFTSIGN) {
+    hipLaunchKernelGGL((act_probe_kernel<ACT_SOFTSIGN, true>), dim3(grid), dim3(256), 0, s, act, z, out, n);
+  } else {
+    hipLaunchKernelGGL((act_probe_kernel<-1, true>), dim3(grid), dim3(256), 0, s, act, z, out, n);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? HPE_OK : hpe_fail(HPE_ERUNTIME, "act_probe launch: %s", hipGetErrorString(e));
 }
 
 extern "C" int hpe_set_exact_fp32(int on) {

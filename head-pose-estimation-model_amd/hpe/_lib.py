@@ -57,6 +57,8 @@ SIGNATURES = {
     'hpe_kernel_timing': (ctypes.c_int, [_i32]),
     'hpe_kernel_times': (ctypes.c_int, [_vp, _i32]),
     'hpe_set_exact_fp32': (ctypes.c_int, [ctypes.c_int]),
+    'hpe_act_probe': (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -302,7 +302,8 @@ def _stage_record(recs):
             return None
     blocks = [f for f in recs if f[BFO_DW]]
     cs = max(f[BFO_COUTP] for f in blocks) + 4           # (cs / 4) odd: conflict-free b128 rows
-    mapf = max(f[BFO_HO] * f[BFO_WO] for f in blocks) * cs
+    # each resident map: a zero row above and below, channel stride coutp + 4 of its writer
+    mapf = max((f[BFO_HO] + 2) * f[BFO_WO] * (f[BFO_COUTP] + 4) for f in blocks)
     wtf = max(f[BFO_COUTP] * f[BFO_KS] for f in recs)
     dwf = max(10 * f[BFO_CINP] for f in blocks)
     lds = 4 * (mapf + wtf + dwf)

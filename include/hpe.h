@@ -250,6 +250,12 @@ int hpe_guard_peek(const hpe_program *prog, int32_t *out);
  * sets the initial value. */
 int hpe_set_exact_fp32(int on);
 
+/* Diagnostics: out[i] = the fused regressor kernels' layer-1 activation `act` (ACT_* of
+ * csrc/hpe_prog.h) of z[i], as they evaluate it (csrc/hpe_dev.h act1_f).  fast = 1: the fp16-split
+ * kernels' form (tanh: fast_tanh5, absolute error <= 2^-22); fast = 0: the exact-fp32 kernels'
+ * (tanh: tanhf).  Device pointers, n floats; asynchronous on `stream`. */
+int hpe_act_probe(int32_t act, int32_t fast, const float *z, float *out, int64_t n, void *stream);
+
 /* Attention heads on H x W > 1 feature maps: the two stages that are not
  * row-local.  Replace the TF kernels behind GlobalAveragePooling2D -> Dense -> Dense -> Multiply
  * (Model-88/attention_model.py:34-38, :78-82) and behind MultiHeadAttention's softmax(QK^T)V over
