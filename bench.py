@@ -17,6 +17,8 @@ Also reported (sub-objects of the one JSON line):
   infer      configs[1]: the selected Model-96 head hrchr82r, batch 256 on 96x96 maps, forward only
   train88    Model-88 create_model on 88x88 maps
   blazeface  configs[4]: unified BlazeFace + both pose heads, batch 1024
+  blazeface_b1  the reference's own detector call (blazeFaceDetectorH5.py:272, :370): latency of one
+             frame (and of 8) per synchronised forward, fused vs per-op plan, CPU oracle beside it
   attn       se_transformer_regr_head (attention_model.py:16-72, checkpoint 12uei1sn: SE + 4-head MHA,
              key_dim 16) on 16x16x88 BlazeFace-tap maps, batch 1024, forward (exact-fp32 MFMA attention
              core, mha_mfma_kernel)
@@ -364,7 +366,10 @@ def bench_p1(keras, batches=(128, 512), n_rows=1 << 20, epochs=3, no_cpu=False):
     try:
         for bs in batches:
             steps = math.ceil(tx.shape[0] / bs)
-            for mode in ('per_step', 'fused_epoch'):
+            # the fused epoch splits a step over hidden units only (<= 12 workgroups at F = 360):
+            # above batch 256 fit runs the per-step launches (FIT_FUSED_AUTO_MAX), so only those
+            # are measured there
+            for mode in ('per_step', 'fused_epoch') if bs <= 256 else ('per_step',):
                 os.environ['HPE_FIT_FUSED'] = '0' if mode == 'per_step' else '1'
                 hpe.set_seed(42)
                 keras.backend.clear_session()
@@ -379,8 +384,9 @@ def bench_p1(keras, batches=(128, 512), n_rows=1 << 20, epochs=3, no_cpu=False):
                     'epoch_s': t_ep, 'steps_per_epoch': steps, 'epochs_timed': len(tm.times) - 1,
                     'fused': bool(getattr(m, '_last_fit_fused', False)),
                     'final_loss': float(m.history.history['loss'][-1])}
-            ps, fe = out['lines']['per_step_b%d' % bs], out['lines']['fused_epoch_b%d' % bs]
-            out['lines']['speedup_b%d' % bs] = ps['us_per_step'] / fe['us_per_step']
+            if bs <= 256:
+                ps, fe = out['lines']['per_step_b%d' % bs], out['lines']['fused_epoch_b%d' % bs]
+                out['lines']['speedup_b%d' % bs] = ps['us_per_step'] / fe['us_per_step']
     finally:
         if prev is None:
             os.environ.pop('HPE_FIT_FUSED', None)
@@ -419,9 +425,10 @@ def bench_p1(keras, batches=(128, 512), n_rows=1 << 20, epochs=3, no_cpu=False):
             os.environ.pop('HPE_FIT_FUSED', None)
         else:
             os.environ['HPE_FIT_FUSED'] = prev
-    # configs[2]: Model-88 create_model, legacy Adam, batch 512 (BASELINE.json), same data
+    # configs[2]: Model-88 create_model, legacy Adam, batch 512 (BASELINE.json), same data; fit runs
+    # it through the per-step launches (batch > FIT_FUSED_AUTO_MAX), the only mode measured
     try:
-        for mode in ('per_step', 'fused_epoch'):
+        for mode in ('per_step',):
             os.environ['HPE_FIT_FUSED'] = '0' if mode == 'per_step' else '1'
             hpe.set_seed(42)
             keras.backend.clear_session()
@@ -571,20 +578,25 @@ def bench_blazeface(dev, iters, no_cpu):
                        'pose heads, reference weights, batch %d frames 128x128x3 (configs[4])' % BLAZE_B,
            'value': BLAZE_B / wall, 'unit': 'images/sec', 'ms_per_batch': wall * 1e3, 'dtype': 'fp32',
            'data': 'synthetic uniform(-1,1) frames',
-           # frac on COMPULSORY bytes (input frame + detector outputs + taps + pose maps, once each);
-           # plan_bytes = what the launches' input / output maps add up to; mfma_frac on the FLOPs
-           'roofline': {'bound': 'hbm', 'achieved': nbytes * BLAZE_B / (ms * 1e-3) / 1e9,
-                        'peak': PEAK_HBM / 1e9, 'unit': 'GB/s',
-                        'frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
+           # 173 FLOP per compulsory byte: compute-bound.  frac on the FLOPs against the ceiling the
+           # pointwise convs run on (fp32 products as 3 fp16 MFMA products: dense fp16 / 3); the HBM
+           # fraction on COMPULSORY bytes (input frame + detector outputs + taps + pose maps, once
+           # each) and on plan_bytes (the launches' input / output maps) beside it
+           'roofline': {'bound': 'mfma', 'achieved': flop * BLAZE_B / (ms * 1e-3) / 1e12,
+                        'peak': PEAK_F16 / 3 / 1e12, 'unit': 'TFLOP/s',
+                        'frac': flop * BLAZE_B / (ms * 1e-3) / (PEAK_F16 / 3),
+                        'peak_basis': 'fp32 products as 3 fp16 MFMA products: 2.5 PFLOP/s dense fp16 / 3 '
+                                      '(depthwise FMAs, a sixth of the FLOPs, run on VALU)',
                         'traffic': _traffic('blazeface'),
+                        'hbm_frac': nbytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
+                        'hbm_achieved_GBps': nbytes * BLAZE_B / (ms * 1e-3) / 1e9,
                         'kernel': 'bf_front_kernel (stem + 64x64 / 32x32 blocks) + bf_stage_kernel (16x16 / 8x8 '
                                   'blocks + detector heads) + 2 pose regressor programs (hpe_blazeface_forward '
                                   '+ hpe_forward), whole forward',
                         'kernel_ms': ms, 'bytes_per_launch': nbytes * BLAZE_B,
                         'plan_bytes': plan_bytes * BLAZE_B,
                         'plan_frac': plan_bytes * BLAZE_B / (ms * 1e-3) / PEAK_HBM,
-                        'flop_per_launch': flop * BLAZE_B,
-                        'mfma_frac': flop * BLAZE_B / (ms * 1e-3) / PEAK_FP32}}
+                        'flop_per_launch': flop * BLAZE_B}}
     if not no_cpu:
         sys.path.insert(0, ROOT)
         from oracle import keras_ref as K
@@ -600,6 +612,58 @@ def bench_blazeface(dev, iters, no_cpu):
         res['cpu_baseline'] = {'value': k * 8 / dt, 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
                                'sample': '%d forwards x 8 frames (oracle/keras_ref.py torch-CPU fp32), %.1f s'
                                          % (k, dt)}
+    return res
+
+
+def bench_blazeface_b1(dev, no_cpu, batches=(1, 8), reps=50):
+    """The reference's own detector call (BlazePoser/blazeFaceDetectorH5.py:272, one frame per call
+    in the webcam loop :370): frames -> detector outputs + poses latency at batch 1 and 8, median of
+    `reps` synchronised forwards, for the default plan (bf_front_kernel + bf_stage_kernel + the two
+    pose programs) and the per-op plan (one launch per layer), beside the oracle's CPU latency."""
+    from hpe import blazeface as BF
+    gdir = os.path.join(ROOT, 'tests', 'golden', 'models')
+    with open(os.path.join(gdir, BLAZE_ID + '.json')) as fh:
+        mc = json.load(fh)['model_config']
+    wts = dict(np.load(os.path.join(gdir, BLAZE_ID + '.npz')))
+    plans = {'fused': BF.BlazeFace(mc, wts, device=dev),
+             'per_op': BF.BlazeFace(mc, wts, device=dev, stage=False, front=False)}
+    res = {'workload': 'unified BlazeFace + stoqa9pt + hrchr82r pose heads, reference weights, one '
+                       'synchronised forward per call (frames -> detector outputs + pose maps)',
+           'unit': 'ms per call (median of %d)' % reps, 'lines': {}}
+    g = torch.Generator(device=dev)
+    g.manual_seed(6)
+    for n in batches:
+        x = (torch.rand((n, 128, 128, 3), generator=g, device=dev) * 2 - 1).contiguous()
+        for name, bf in plans.items():
+            for _ in range(5):
+                bf.forward(x)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                bf.forward(x)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            ms = 1e3 * float(np.median(ts))
+            res['lines']['%s_b%d' % (name, n)] = {'ms': ms, 'frames_per_sec': n / ms * 1e3}
+    res['value_ms_b1'] = min(res['lines']['fused_b1']['ms'], res['lines']['per_op_b1']['ms'])
+    res['plan_b1'] = 'fused' if res['lines']['fused_b1']['ms'] <= res['lines']['per_op_b1']['ms'] else 'per_op'
+    if not no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import keras_ref as K
+        gr = K.Graph(mc, wts, dtype=torch.float32)
+        xs = np.random.default_rng(1).uniform(-1, 1, (1, 128, 128, 3)).astype(np.float32)
+        threads, _ = _threads_for_cpu(lambda: gr.forward(xs))
+        ts = []
+        t_end = time.perf_counter() + 5.0
+        while time.perf_counter() < t_end or len(ts) < 3:
+            t0 = time.perf_counter()
+            gr.forward(xs)
+            ts.append(time.perf_counter() - t0)
+        res['cpu_baseline'] = {'value': 1e3 * float(np.median(ts)), 'unit': 'ms per frame (batch 1)',
+                               'cores': threads, 'kind': 'port',
+                               'sample': '%d batch-1 forwards (oracle/keras_ref.py torch-CPU fp32), median'
+                                         % len(ts)}
     return res
 
 
@@ -731,7 +795,7 @@ def parse(argv):
     ap.add_argument('--no-strong', action='store_true')
     ap.add_argument('--no-p1', action='store_true')
     ap.add_argument('--no-attn', action='store_true')
-    ap.add_argument('--only', default='', help='comma list of lines to run (train,strong,p1,infer,train88,blazeface,attn)')
+    ap.add_argument('--only', default='', help='comma list of lines to run (train,strong,p1,infer,train88,blazeface,blazeface_b1,attn)')
     return ap.parse_args(argv)
 
 
@@ -819,6 +883,8 @@ def main(argv=None):
         out['attn'] = bench_attn(dev, max(10, a.steps))
     if rank == 0 and want('blazeface', a.no_blaze):
         out['blazeface'] = bench_blazeface(dev, max(10, a.steps), a.no_cpu or world > 1)
+    if rank == 0 and want('blazeface_b1', a.no_blaze):
+        out['blazeface_b1'] = bench_blazeface_b1(dev, a.no_cpu or world > 1)
     if rank == 0 and world == 1 and want('train') and not a.no_cpu:
         cb = cpu_baseline((m.model_config, init_w))
         out['cpu_baseline'] = cb

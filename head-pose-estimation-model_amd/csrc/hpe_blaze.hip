@@ -1658,7 +1658,11 @@ static int check_front(const int* f, int i, int rest) {
   struct { int s, cinp, coutp, h, ho, padt, res; } L[6] = {
       {0}, {1, 24, 24, 64, 64, 1, BF_RES_ID}, {1, 24, 32, 64, 64, 1, BF_RES_ID}, {2, 32, 32, 64, 32, 0, BF_RES_MAXPOOL},
       {1, 32, 40, 32, 32, 1, BF_RES_ID}, {1, 40, 48, 32, 32, 1, BF_RES_ID}};
+  // bf_front_kernel keeps the stem's and blocks 1-4's maps in LDS rings (never in HBM): each of
+  // them must go to a workspace buffer (not a caller output), and no record after the front may
+  // read it (checked below over the rest of the plan)
   int last = g[BFO_DST];
+  if (last != BF_BUF_A && last != BF_BUF_B) return hpe_fail(HPE_EINVAL, "blazeface front %d: stem output buffer", i);
   for (int k = 1; k <= 5; ++k) {
     const int* b = f + (k + 1) * BFO_WORDS;
     if ((b[BFO_KIND] != BF_ROWS && b[BFO_KIND] != BF_BLOCK) || !b[BFO_DW] || !b[BFO_RELU] || b[BFO_SPLIT] ||
@@ -1667,8 +1671,25 @@ static int check_front(const int* f, int i, int rest) {
         b[BFO_PADL] != L[k].padt || b[BFO_RES] != L[k].res || b[BFO_SRC] != last || b[BFO_OSTRIDE] != L[k].coutp)
       return hpe_fail(HPE_EINVAL, "blazeface front %d: block %d geometry", i, k);
     last = b[BFO_DST];
+    if (last != BF_BUF_A && last != BF_BUF_B) return hpe_fail(HPE_EINVAL, "blazeface front %d: block %d output buffer", i, k);
   }
-  if (last != BF_BUF_A && last != BF_BUF_B) return hpe_fail(HPE_EINVAL, "blazeface front %d: output buffer", i);
+  // after the front only block 5's map is in a ping-pong buffer: the other buffer holds no map
+  // until a later record writes it (a stage reads HBM in its first op only, its blocks' maps stay
+  // in LDS: they write nothing)
+  const int other = last == BF_BUF_A ? BF_BUF_B : BF_BUF_A;
+  bool other_ok = false;
+  for (int k = 7; k <= rest; ++k) {
+    const int* r = f + k * BFO_WORDS;
+    if (r[BFO_KIND] == BF_STAGE) {
+      if (k + 1 <= rest && (r + BFO_WORDS)[BFO_SRC] == other && !other_ok)
+        return hpe_fail(HPE_EINVAL, "blazeface front %d: record %d reads a map the front keeps in LDS", i, i + k + 1);
+      k += r[BFO_NI];
+      continue;
+    }
+    if (r[BFO_SRC] == other && !other_ok)
+      return hpe_fail(HPE_EINVAL, "blazeface front %d: record %d reads a map the front keeps in LDS", i, i + k);
+    if (r[BFO_DST] == other || (r[BFO_SPLIT] && r[BFO_DST2] == other)) other_ok = true;
+  }
   return 0;
 }
 

@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -1031,7 +1032,9 @@ bool hpe_exact_fp32() {
 // events are created up front by hpe_kernel_timing, so recording never allocates
 static std::vector<hipEvent_t> g_tev;
 static int g_tev_cap = 0;
-static std::atomic<int> g_tev_n{0};
+static std::atomic<int> g_tev_n{0};             // slots reserved (hpe_tev_begin)
+static std::unique_ptr<std::atomic<uint8_t>[]> g_tev_ok;  // slot's end event recorded (hpe_tev_end)
+static int g_tev_ok_cap = 0;
 static bool g_tev_on = false;
 
 // reserves the next event pair (launch() may run on several host threads): the slot to pass to
@@ -1048,7 +1051,9 @@ int hpe_tev_begin(hipStream_t s) {
 }
 // called on every path after hpe_tev_begin, failed launches included, so no slot stays half-recorded
 void hpe_tev_end(hipStream_t s, int slot) {
-  if (slot >= 0) hipEventRecord(g_tev[2 * slot + 1], s);
+  if (slot < 0) return;
+  hipEventRecord(g_tev[2 * slot + 1], s);
+  g_tev_ok[slot].store(1, std::memory_order_release);
 }
 
 extern "C" int hpe_kernel_timing(int32_t capacity) {
@@ -1060,6 +1065,11 @@ extern "C" int hpe_kernel_timing(int32_t capacity) {
     HIPCHK(hipEventCreate(&e));
     g_tev.push_back(e);
   }
+  if (g_tev_ok_cap < capacity) {
+    g_tev_ok.reset(new std::atomic<uint8_t>[capacity]);
+    g_tev_ok_cap = capacity;
+  }
+  for (int i = 0; i < capacity; ++i) g_tev_ok[i].store(0, std::memory_order_relaxed);
   g_tev_cap = capacity;
   g_tev_on = true;
   return HPE_OK;
@@ -1067,7 +1077,11 @@ extern "C" int hpe_kernel_timing(int32_t capacity) {
 
 extern "C" int hpe_kernel_times(float* ms, int32_t max) {
   if (!ms && max > 0) return fail(HPE_EINVAL, "hpe_kernel_times: null argument");
-  const int done = g_tev_n.load(std::memory_order_relaxed);
+  // the leading run of slots whose end event is recorded (a slot another host thread reserved but
+  // has not closed yet ends the run: its end event does not exist yet)
+  const int reserved = g_tev_n.load(std::memory_order_relaxed);
+  int done = 0;
+  while (done < reserved && done < g_tev_cap && g_tev_ok[done].load(std::memory_order_acquire)) ++done;
   const int n = done < max ? done : max;
   for (int i = 0; i < n; ++i) {
     HIPCHK(hipEventSynchronize(g_tev[2 * i + 1]));
@@ -1530,7 +1544,8 @@ extern "C" int hpe_fit_steps_dp(const hpe_program* p, float* params, float* para
                                 float x_bound, int32_t kind, float lr, float b1, float b2, float eps,
                                 uint64_t seed_base, int64_t iter0, void* ws, float* grad, float* stats,
                                 int32_t stats_stride, int32_t rank, int32_t world, hpe_allreduce_fn allreduce,
-                                void* user, void* stream) {
+                                void* user, int64_t* steps_done, void* stream) {
+  if (steps_done) *steps_done = 0;
   if (!p || !params || !x || !ytrue || !perm || !ws || !grad || !l2 || !tpos || !stats || !allreduce)
     return fail(HPE_EINVAL, "hpe_fit_steps_dp: null argument");
   if (n <= 0 || batch <= 0 || P <= 0 || iter0 < 0 || world < 1 || rank < 0 || rank >= world)
@@ -1562,6 +1577,7 @@ extern "C" int hpe_fit_steps_dp(const hpe_program* p, float* params, float* para
     rc = hpe_optim_step(kind, lr, b1, b2, eps, it, 1.f, params, params_t, m, v, grad, l2, tpos, n_train,
                         stats + st * stats_stride, stream);
     if (rc) return rc;
+    if (steps_done) *steps_done = st + 1;  // optimizer steps applied: the caller's iteration count
   }
   return HPE_OK;
 }

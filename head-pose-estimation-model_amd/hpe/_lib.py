@@ -31,7 +31,7 @@ SIGNATURES = {
                                      _f, _i32, _f, _f, _f, _f, _u64, _i64, _vp, _vp, _vp, _i32, _vp]),
     'hpe_fit_steps_dp': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32,
                                         _f, _i32, _f, _f, _f, _f, _u64, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
-                                        _vp, _vp, _vp]),
+                                        _vp, _vp, _vp, _vp]),
     'hpe_fit_supported': (ctypes.c_int, [_vp, _i32]),
     'hpe_fit_workspace_size': (_sz, [_vp, _i32]),
     'hpe_fit_epoch': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f,

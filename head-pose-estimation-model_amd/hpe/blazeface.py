@@ -357,6 +357,8 @@ def _with_front(ops):
                                    g[BFO_PADT], g[BFO_PADL], g[BFO_SRC]) != (128, 128, 64, 64, 24, 2, 1, 1, BUF_IMG)):
         return ops
     last = g[BFO_DST]
+    if last not in (BUF_A, BUF_B):       # the front keeps the stem's map in LDS only
+        return ops
     for b, (s, cinp, coutp, h, ho, pad, res) in zip(ops[1:6], _FRONT_BLOCKS):
         if (b[BFO_KIND] not in (BF_ROWS, BF_BLOCK) or not b[BFO_DW] or not b[BFO_RELU] or b[BFO_SPLIT] or
                 (b[BFO_STRIDE], b[BFO_CINP], b[BFO_COUTP], b[BFO_H], b[BFO_W], b[BFO_HO], b[BFO_WO], b[BFO_PADT],
@@ -364,8 +366,14 @@ def _with_front(ops):
                 or b[BFO_SRC] != last):
             return ops
         last = b[BFO_DST]
-    if last not in (BUF_A, BUF_B):
-        return ops
+        if last not in (BUF_A, BUF_B):   # blocks 1-4: LDS only; block 5: the workspace map it writes
+            return ops
+    # the record after the front must read block 5's map (the others never reach HBM)
+    nxt = ops[6] if len(ops) > 6 else None
+    if nxt is not None:
+        rec = ops[7] if nxt[BFO_KIND] == BF_STAGE and len(ops) > 7 else nxt
+        if rec[BFO_SRC] != last:
+            return ops
     f = [0] * BFO_WORDS
     f[BFO_KIND], f[BFO_NI], f[BFO_LDS] = BF_FRONT, 6, FRONT_LDS
     return [f] + ops

@@ -251,6 +251,7 @@ class Engine:
                     errors.append(e)
                     return 1
             hook = self.ALLREDUCE_FN(allreduce)
+            done = ctypes.c_int64(0)
             rc = lib.hpe_fit_steps_dp(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
                                       _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),
                                       n, int(batch), int(P), float(x_bound), kind, float(opt.learning_rate),
@@ -258,12 +259,15 @@ class Engine:
                                       int(seed_base) & 0xFFFFFFFFFFFFFFFF, int(self.iterations), _ptr(ws),
                                       _ptr(self.grad), _ptr(stats), int(stats.shape[1]),
                                       mod.get_rank(grp), mod.get_world_size(grp),
-                                      ctypes.cast(hook, ctypes.c_void_p), None, _stream())
+                                      ctypes.cast(hook, ctypes.c_void_p), None, ctypes.byref(done), _stream())
+            # the steps whose optimizer update was applied advance the iteration count even when
+            # the epoch stopped early (Adam's bias correction and the dropout seeds of a retry stay
+            # in step with params / m / v)
+            self._pending = None
+            self.iterations += int(done.value)
             if errors:
                 raise errors[0]
             _lib.check(rc, 'hpe_fit_steps_dp')
-            self._pending = None
-            self.iterations += steps
             return
         _lib.check(lib.hpe_fit_steps(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
                                      _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),

@@ -137,7 +137,9 @@ int hpe_fit_steps(const hpe_program *prog, float *params, float *params_t, float
  * stream, user) — the caller's sum over ranks, e.g. an RCCL all-reduce on that stream; non-zero
  * aborts with HPE_ERUNTIME — then hpe_optim_step with iteration iter0 + 1 + s into
  * stats + s * stats_stride (stats_stride >= 2 + hpe_optim_grid(n_train)).  Bit-identical to the
- * per-step launches issued one by one. */
+ * per-step launches issued one by one.  steps_done (may be NULL) receives the number of steps whose
+ * optimizer update was issued, also when the epoch stops early on an error (the caller advances its
+ * iteration count by it). */
 typedef int (*hpe_allreduce_fn)(float *buf, int64_t n, void *stream, void *user);
 int hpe_fit_steps_dp(const hpe_program *prog, float *params, float *params_t, float *m, float *v,
                      const float *l2, const int32_t *tpos, int64_t n_train, const float *x,
@@ -145,7 +147,7 @@ int hpe_fit_steps_dp(const hpe_program *prog, float *params, float *params_t, fl
                      float x_bound, int32_t kind, float lr, float beta_1, float beta_2, float epsilon,
                      uint64_t seed_base, int64_t iter0, void *workspace, float *grad, float *stats,
                      int32_t stats_stride, int32_t rank, int32_t world, hpe_allreduce_fn allreduce,
-                     void *user, void *stream);
+                     void *user, int64_t *steps_done, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
@@ -232,7 +234,9 @@ const char *hpe_build_id(void);
  * the next `capacity` program launches (0 turns it off): hpe_forward / hpe_train_step record a HIP
  * event pair on their stream around the launch's dominant kernel only (the fp16-split kernel, not
  * its early-exit exact twin, nor hpe_reduce).  hpe_kernel_times waits for the recorded pairs and
- * writes their elapsed milliseconds to ms[0 .. n); returns n (<= max). */
+ * writes their elapsed milliseconds to ms[0 .. n); returns n (<= max): the leading run of pairs
+ * whose launch has finished recording (a launch another host thread has not returned from yet
+ * ends the run). */
 int hpe_kernel_timing(int32_t capacity);
 int hpe_kernel_times(float *ms, int32_t max);
 

@@ -172,7 +172,11 @@ def test_capi_validates_front_record():
     base = B.BFH_WORDS
     for off, val in ((B.BFO_NI, 5), (B.BFO_LDS, 100_000), (B.BFO_WORDS + B.BFO_COUT, 16),
                      (3 * B.BFO_WORDS + B.BFO_COUTP, 40), (4 * B.BFO_WORDS + B.BFO_STRIDE, 1),
-                     (6 * B.BFO_WORDS + B.BFO_DST, B.BUF_OUT0)):
+                     (6 * B.BFO_WORDS + B.BFO_DST, B.BUF_OUT0),
+                     # an intermediate map the front keeps in LDS sent to a caller output
+                     (1 * B.BFO_WORDS + B.BFO_DST, B.BUF_OUT0), (3 * B.BFO_WORDS + B.BFO_DST, B.BUF_OUT0 + 1),
+                     # ... or read by the record after the front (block 4's map, never in HBM)
+                     (8 * B.BFO_WORDS + B.BFO_SRC, int(words[base + 5 * B.BFO_WORDS + B.BFO_DST]))):
         bad = words.copy()
         bad[base + off] = val
         assert lib.hpe_blazeface_create(bad.ctypes.data_as(ctypes.c_void_p), bad.size, ctypes.byref(h)) == 1, off

@@ -87,9 +87,19 @@ def _dp_worker(rank, world, port, out):
         m.compile(optimizer=kk.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
         h = m.fit(f_(160, 96, seed=21), lb(160, seed=22), batch_size=64, epochs=2, shuffle=True, verbose=0)
         res[mode] = (np.asarray(h.history['loss']), m.weights_dict())
+        # 129 rows at batch 64 on 2 ranks: the last batch has ONE row, so rank 0's share
+        # is empty (hpe_fit_steps_dp's zeroed-gradient branch) while rank 1 trains on it
+        H.set_seed(4)
+        m2 = H.model_from_config(mc, w).distribute()
+        m2.compile(optimizer=kk.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
+        h2 = m2.fit(f_(129, 96, seed=23), lb(129, seed=24), batch_size=64, epochs=2, shuffle=True, verbose=0)
+        res[mode + 'r'] = (np.asarray(h2.history['loss']), m2.weights_dict())
+        assert m2._eng().iterations == 6
     os.environ.pop('HPE_FIT_STEPS')
-    same = all(np.array_equal(res['1'][1][k], v) for k, v in res['0'][1].items())
-    same = same and np.array_equal(res['1'][0], res['0'][0])
+    same = True
+    for key in ('', 'r'):
+        same = same and all(np.array_equal(res['1' + key][1][k], v) for k, v in res['0' + key][1].items())
+        same = same and np.array_equal(res['1' + key][0], res['0' + key][0])
     if rank == 0:
         h, wd = res['1']
         np.savez(out, loss=h, c_equals_python=same, **{k.replace('/', '|'): v for k, v in wd.items()})
