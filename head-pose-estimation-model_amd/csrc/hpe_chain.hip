@@ -19,6 +19,41 @@
 #define CHAIN_KH 48                     // rows of 24 16-B chunks: 88- or 96-channel inputs
 #define CHAIN_XF (32 * CHAIN_KH * 2)    // floats per wave X tile
 #define CHAIN_TAB 1280                  // floats of shared weight tables per workgroup
+// cache policy of the X stream's LDS-DMA (read once): non-temporal (aux 2).  The access pattern
+// alone (scripts/stream_probe.hip: 12 waves x one 12-KiB tile in flight, MI355X) streams at
+// 7.0 TB/s nt vs 6.1 TB/s with the default policy
+#ifndef CHAIN_AUX
+#define CHAIN_AUX 2
+#endif
+#ifndef CHAIN_PROBE
+#define CHAIN_PROBE 0   // diagnostics builds: 1 = no output stores, 2 = no arithmetic (stream only)
+#endif
+// the split kernel's X ring: CHAIN_SNW waves per workgroup, each with CHAIN_SD tile slots; a slot
+// is refilled (the tile CHAIN_SD ahead) as soon as layer 1 has read it, so that load streams in
+// during the rest of the tile's arithmetic (layer 2, activations, head).  Waiting for a tile only
+// once the previous one was completely done serialised each load behind the arithmetic: 4.4 TB/s
+// against 7.0 TB/s for the stream alone (scripts/stream_probe.hip, CHAIN_PROBE=2 builds).  Fewer
+// waves with more slots each (4 x 3, 6 x 2) measured slower: one wave per SIMD leaves the
+// arithmetic's own latency exposed.
+#ifndef CHAIN_SNW
+#define CHAIN_SNW 12
+#endif
+#ifndef CHAIN_SD
+#define CHAIN_SD 1
+#endif
+static_assert(4 * (CHAIN_TAB + CHAIN_SNW * CHAIN_SD * CHAIN_XF) <= 160 * 1024, "chain split ring exceeds LDS");
+
+// s_waitcnt vmcnt(n) for the split kernel's ring: n = 12 x the tiles issued after the one waited
+// for (the output stores, younger still and of a compiler-chosen instruction count, are left out:
+// the wait then also retires them, never too few pieces)
+__device__ __forceinline__ void chain_vm_wait(int n) {
+  switch (n) {
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
@@ -187,7 +222,7 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
 // non-finite (an input or activation outside the fp16 range) sets the guard word; the exact-fp32
 // kernel launched behind it then recomputes the whole launch.
 template <int A1, int A2, int A3, int GATHER>
-__global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
+__global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* prog = args.prog;
   const int* o = prog + prog[H_OPS_OFF];
@@ -200,8 +235,44 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
   float* tb2 = tb1 + 32;
   float* tw3 = tb2 + 32;
   float* tb3 = tw3 + 128;
-  float* xs = lds + CHAIN_TAB + wave * CHAIN_XF;
+  float* ring = lds + CHAIN_TAB + wave * (CHAIN_SD * CHAIN_XF);
   const int Fh = F2 > 0 ? F2 : F1;
+  const int64_t nrows = args.nrows;
+  const int64_t ntiles = (nrows + 31) / 32;
+  const int P = args.P;
+  const int64_t gw = (int64_t)blockIdx.x * CHAIN_SNW + wave;
+  const int64_t nw = (int64_t)gridDim.x * CHAIN_SNW;
+  // HBM -> LDS slot d: 12 x 1 KiB global_load_lds, swizzled source chunks, rows past the end repeat
+  // the last row; per-lane (row, chunk) recomputed per tile from an opaque lane id (cheap VALU)
+  auto issue = [&](int64_t tile, int d) {
+    const int64_t row0 = tile * 32;
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
+    const float* xt = args.x + row0 * Cin;
+    float* xs = ring + d * CHAIN_XF;
+#pragma unroll
+    for (int pc = 0; pc < 12; ++pc) {
+      const int slot = pc * 64 + lz;
+      const int r = slot / 24, ph = slot - r * 24;
+      const int c = csw(r, ph);
+      const int cc = 4 * c < Cin ? c : 0;
+      const int rr = min(r, last);
+      const float* src;
+      if (GATHER) {
+        const int64_t R = row0 + rr;
+        const int64_t img = R / P, pos = R - img * P;
+        src = args.x + ((int64_t)args.idx[img] * P + pos) * Cin + 4 * cc;
+      } else {
+        src = xt + (rr * Cin + 4 * cc);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + pc * 256), 16, 0, CHAIN_AUX);
+    }
+  };
+  // the ring's first tiles go out before the weight prologue
+#pragma unroll
+  for (int d = 0; d < CHAIN_SD; ++d)
+    if (gw + d * nw < ntiles) issue(gw + d * nw, d);
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
     const int nn = i >> 5, m = i & 31;
     tw2[i] = (F2 > 0 && nn < F1 && m < F2) ? P_[o[O_AUX0] + nn * F2 + m] : 0.f;
@@ -263,36 +334,39 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
 #pragma unroll
   for (int g = 0; g < 16; ++g) b1r[g] = tb1[(g & 3) + 8 * (g >> 2) + 4 * half];
 
-  const int64_t nrows = args.nrows;
-  const int64_t ntiles = (nrows + 31) / 32;
-  const int P = args.P;
-  const int64_t gw = (int64_t)blockIdx.x * CHAIN_NW + wave;
-  const int64_t nw = (int64_t)gridDim.x * CHAIN_NW;
   bool bad = false;
-  for (int64_t tile = gw; tile < ntiles; tile += nw) {
-    const int64_t row0 = tile * 32;
-    int lz = lane;
-    asm volatile("" : "+v"(lz));
-    const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
-    const float* xt = args.x + row0 * Cin;
-#pragma unroll
-    for (int pc = 0; pc < 12; ++pc) {
-      const int slot = pc * 64 + lz;
-      const int r = slot / 24, ph = slot - r * 24;
-      const int c = csw(r, ph);
-      const int cc = 4 * c < Cin ? c : 0;
-      const int rr = min(r, last);
-      const float* src;
-      if (GATHER) {
-        const int64_t R = row0 + rr;
-        const int64_t img = R / P, pos = R - img * P;
-        src = args.x + ((int64_t)args.idx[img] * P + pos) * Cin + 4 * cc;
-      } else {
-        src = xt + (rr * Cin + 4 * cc);
-      }
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + pc * 256), 16, 0, 0);
+  int d = 0;
+  int64_t pr = 0;          // the previous tile's outputs (row of this lane, 3 values), stored late
+  float pv0 = 0.f, pv1 = 0.f, pv2 = 0.f;
+  auto store_prev = [&]() {
+#if CHAIN_PROBE == 1
+    if (pv0 == 1234.5f)
+#endif
+    if (half == 0 && pr < nrows) {
+      float* yp = args.y + pr * 3;
+      yp[0] = pv0;
+      yp[1] = pv1;
+      yp[2] = pv2;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // GATHER: the index loads of a tile's issue are vector loads too, waited for by the compiler
+  // (vmcnt(0)): the ring then drains at each issue, still correct
+  for (int64_t tile = gw, k = 0; tile < ntiles; tile += nw, ++k, d = d + 1 == CHAIN_SD ? 0 : d + 1) {
+    const int64_t row0 = tile * 32;
+    // wait for this tile: the pieces of the tiles after it already issued (the ring's other
+    // slots) stay in flight
+    {
+      int younger = 0;
+#pragma unroll
+      for (int j = 1; j < CHAIN_SD; ++j) younger += tile + j * nw < ntiles ? 12 : 0;
+      chain_vm_wait(younger);
+    }
+    const float* xs = ring + d * CHAIN_XF;
+#if CHAIN_PROBE == 2
+    if (xs[lane] == 1234.5f) args.y[0] = 1.f;
+    if (tile + CHAIN_SD * nw < ntiles) issue(tile + CHAIN_SD * nw, d);
+    continue;
+#endif
     // ---- layer 1: B = X^T, lane (row l32, half h) holds X[row][16 s + 8 h .. + 8) ----
     const float* xr = xs + l32 * 96;
     const int sw = (l32 >> 1) & 7;
@@ -304,6 +378,12 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
       const f32x4 a1 = *(const f32x4*)(xr + 4 * ((c0 + 1) ^ sw));
       acc = mfma3_wd(w1[s], split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), acc);
     }
+    // the slot's reads are consumed by the MFMAs above: the previous tile's outputs go out, then
+    // the tile CHAIN_SD ahead streams into this slot during the rest of this tile's arithmetic
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if (k > 0) store_prev();
+    if (tile + CHAIN_SD * nw < ntiles) issue(tile + CHAIN_SD * nw, d);
     float chk = sum16(acc);
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, fmaf(acc[g], inv1, b1r[g]));
@@ -340,14 +420,14 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_split_kernel(Args args) {
     s0 += __shfl_xor(s0, 32, 64);
     s1 += __shfl_xor(s1, 32, 64);
     s2 += __shfl_xor(s2, 32, 64);
-    const int64_t R = row0 + l32;
-    if (half == 0 && R < nrows) {
-      float* yp = args.y + R * 3;
-      yp[0] = cact<A3>(act3, s0 + tb3[0]);
-      yp[1] = cact<A3>(act3, s1 + tb3[1]);
-      yp[2] = cact<A3>(act3, s2 + tb3[2]);
-    }
+    // this tile's outputs leave with the next tile's layer 1 (a store issued here would be the
+    // youngest memory operation at the next tile's wait, and waited for)
+    pr = row0 + l32;
+    pv0 = cact<A3>(act3, s0 + tb3[0]);
+    pv1 = cact<A3>(act3, s1 + tb3[1]);
+    pv2 = cact<A3>(act3, s2 + tb3[2]);
   }
+  if (gw < ntiles) store_prev();
   if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -360,6 +440,7 @@ int chain_supported(const int* w) {
 }
 
 int chain_lds_bytes() { return (CHAIN_TAB + CHAIN_NW * CHAIN_XF) * 4; }
+static int chain_split_lds_bytes() { return (CHAIN_TAB + CHAIN_SNW * CHAIN_SD * CHAIN_XF) * 4; }
 
 int chain_grid_cap(int n_cu) { return n_cu; }  // one 12-wave workgroup per CU (LDS ~149 KiB)
 
@@ -375,9 +456,10 @@ static chain_fn pick(const int* o, bool gather) {
   return gather ? K<-1, -1, -1, 1>::f : K<-1, -1, -1, 0>::f;
 }
 
-static int launch_one(chain_fn k, const Args& a, int grid, hipStream_t s) {
-  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, chain_lds_bytes());
-  hipLaunchKernelGGL(k, dim3(grid), dim3(CHAIN_NW * 64), chain_lds_bytes(), s, a);
+static int launch_one(chain_fn k, const Args& a, int grid, hipStream_t s, bool split = false) {
+  const int lds = split ? chain_split_lds_bytes() : chain_lds_bytes();
+  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(k, dim3(grid), dim3((split ? CHAIN_SNW : CHAIN_NW) * 64), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -395,7 +477,7 @@ int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
     return rc;
   }
   const int tv = hpe_tev_begin(s);
-  const int rc = launch_one(pick<ChainSplit>(o, g), a, grid, s);
+  const int rc = launch_one(pick<ChainSplit>(o, g), a, grid, s, true);
   hpe_tev_end(s, tv);
   if (rc) return rc;
   return launch_one(pick<ChainExact>(o, g), a, grid, s);
