@@ -1332,7 +1332,32 @@ __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
       for (int nc = 0; nc < NC; ++nc) acc[nc] = mfma_split(av, wr[nc][k], acc[nc]);
     }
   }
-  // epilogue: lane = output channel, register g = position 32 c + 4 half + (g & 3) + 8 (g >> 2)
+  // epilogue: lane = output channel, register g = position 32 c + 4 half + (g & 3) + 8 (g >> 2).
+  // Every residual read of the row is issued before the first output write: the writes go to the
+  // next layer's ring in the same LDS array, which the compiler cannot tell apart from this ring, so
+  // read-write-read-... interleaved put each read behind its own lgkmcnt(0) (an LDS round trip per
+  // output register; round 6)
+#ifndef BFF_RESB
+#define BFF_RESB 1
+#endif
+  float res[NC][16];
+  if (BFF_RESB && !zero) {
+#pragma unroll
+    for (int nc = 0; nc < NC; ++nc) {
+      const int n = min(nc * 32 + l32, L::CINP - 1);  // n >= CINP: read a valid address, unused
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int x = 32 * c + 4 * half + (g & 3) + 8 * (g >> 2);
+        if (L::S == 1) {
+          res[nc][g] = ring[(oy & 3) * ROW + (x + L::PADL) * L::CS + n];
+        } else {
+          const float* t0 = ring + ((2 * oy) & 3) * ROW + 2 * x * L::CS + n;
+          const float* t1 = ring + ((2 * oy + 1) & 3) * ROW + 2 * x * L::CS + n;
+          res[nc][g] = fmaxf(fmaxf(t0[0], t0[L::CS]), fmaxf(t1[0], t1[L::CS]));
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) {
     const int n = nc * 32 + l32;
@@ -1344,7 +1369,9 @@ __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
       if (!zero) {
         v = acc[nc][g] + bias[nc];
         if (n < L::CINP) {
-          if (L::S == 1) {
+          if (BFF_RESB) {
+            v += res[nc][g];
+          } else if (L::S == 1) {
             v += ring[(oy & 3) * ROW + (x + L::PADL) * L::CS + n];
           } else {
             const float* t0 = ring + ((2 * oy) & 3) * ROW + 2 * x * L::CS + n;

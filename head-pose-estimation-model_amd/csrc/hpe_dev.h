@@ -12,9 +12,15 @@
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
+// HPE_GLDS_NT: the X stream's pieces non-temporal (read once per launch)
+#ifdef HPE_GLDS_NT
+#define HPE_GLDS16_OP "global_load_lds_dwordx4 %1, off nt"
+#else
+#define HPE_GLDS16_OP "global_load_lds_dwordx4 %1, off"
+#endif
 __device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_dst) {
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" HPE_GLDS16_OP "\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 __device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_dst) {
