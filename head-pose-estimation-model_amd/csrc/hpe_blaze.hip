@@ -772,8 +772,8 @@ __device__ __forceinline__ float dpp_from_next(float v) {  // lane i <- lane i +
 #else
 #define BFS_SB() do {} while (0)
 #endif
-// the streamed maps (the stage's source rows, taps and head outputs, each touched once) bypass
-// L2 retention (non-temporal), so the stage's weights, re-read by every frame, stay L2-resident
+// the streamed maps (the stage's source rows and the taps, each touched once) bypass L2 retention
+// (non-temporal), so the stage's weights, re-read by every frame, stay L2-resident
 #ifndef BFS_NT
 #define BFS_NT 1
 #endif
@@ -785,10 +785,7 @@ __device__ __forceinline__ void st4_nt(float* p, f32x4 v) {
   if (BFS_NT) __builtin_nontemporal_store(v, (f32x4*)p);
   else *(f32x4*)p = v;
 }
-__device__ __forceinline__ void st1_nt(float* p, float v) {
-  if (BFS_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+
 
 // the prefetched reads of one K-step (8 input channels; this lane's quad c0 = 4 half + 8 k); the
 // depthwise table rows (10 broadcast quads) are read inside the step, ahead of the taps' DPP work
@@ -1034,11 +1031,13 @@ __device__ __forceinline__ void bfs_store(const BfSub& o, const float* const* bu
       const int q = chunk * 32 + (g & 3) + 8 * (g >> 2) + 4 * half;
       const float v = acc[j][g];
       const int64_t pos = img * hwo + q;
+      // plain stores: 4-B non-temporal stores of these scattered head outputs reach HBM as partial
+      // lines (the stage's PMC write bytes 216 MB with them, 190 MB without)
       if (split) {
-        if (n < split) st1_nt(gd + pos * split + n, v);
-        else if (n < cout) st1_nt(gd2 + pos * (cout - split) + (n - split), v);
+        if (n < split) gd[pos * split + n] = v;
+        else if (n < cout) gd2[pos * (cout - split) + (n - split)] = v;
       } else if (n < ostride) {
-        st1_nt(gd + pos * ostride + n, v);
+        gd[pos * ostride + n] = v;
       }
     }
   }

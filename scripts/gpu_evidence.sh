@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 SKIP_TESTS=${SKIP_TESTS:-0}
 step() { echo "[$(date +%T)] $*"; }
 step smoke
@@ -20,10 +20,15 @@ step bench
 timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 cat gpurun_out/bench_$TAG.json
 if [ "${PROFILE:-1}" = 1 ]; then
-  for line in ${LINES:-train infer train88 blazeface}; do
+  for line in ${LINES:-train infer train88 blazeface blazeface_b1 p1 attn}; do
     step "trace $line"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$line -o trace --output-format csv -- \
       python3 bench.py --only $line --no-cpu --steps 10 --warmup 2 > gpurun_out/prof_${TAG}_$line.log 2>&1 || exit $?
+  done
+fi
+if [ "${PMC:-1}" = 1 ]; then
+  for line in ${PMC_LINES:-train train88 infer blazeface}; do
+    TAG=$TAG LINE=$line scripts/pmc_line.sh || exit $?
   done
 fi
 step done
