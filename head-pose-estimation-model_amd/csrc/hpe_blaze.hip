@@ -767,6 +767,9 @@ __device__ __forceinline__ float dpp_from_next(float v) {  // lane i <- lane i +
 #ifndef BFS_PIPE
 #define BFS_PIPE 0   // 1: the K loop prefetches the next step's taps / W^T (more VGPRs: spills)
 #endif
+#ifndef BFS_PIPE1
+#define BFS_PIPE1 0  // 1: the same for the single-chunk (NC = 1) tasks only (8x8 ops, heads): neutral
+#endif
 #ifdef BFS_SB_ON   // a scheduling barrier after each step's reads (measured slower: more spills)
 #define BFS_SB() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -908,7 +911,7 @@ __device__ __forceinline__ void bfs_task(const BfSub& o, const float* src, int s
   const int nks = cinp >> 3;
   int c0 = 4 * half;
   Dv dv;
-  if constexpr (V == BFV_BAND || V == BFV_GLOBAL || !BFS_PIPE) {
+  if constexpr (V == BFV_BAND || V == BFV_GLOBAL || !(BFS_PIPE || (BFS_PIPE1 && NC == 1))) {
     for (int k = 0; k < nks; ++k, c0 += 8) {
       K A;
       load_dw(c0, dv);

@@ -36,6 +36,9 @@
 namespace MLP2_NS {
 
 #define MLP2_MAXW 12          // waves per workgroup (hidden width <= 384)
+#ifndef MLP2_BAR1_SKIP
+#define MLP2_BAR1_SKIP 1   // 0: the first barrier on every tile (round 5), for A/B
+#endif
 #ifndef MLP2_W88
 #define MLP2_W88 2
 #endif
@@ -384,7 +387,12 @@ __global__ void __launch_bounds__(NWM * 64) __attribute__((amdgpu_waves_per_eu(N
     // split before this barrier, the raw buffer is free)
     if constexpr (!PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(0);
-    bar_lds();
+    // PRE with the head-shadow pre-split (NCB >= 4): every LDS hazard this barrier guards is already
+    // ordered by the previous tile's third barrier — the raw tile was split (and the next raw tile's
+    // landing waited for) before it, xf / the partials / this parity's labels were last read before
+    // it, the A1 park and the loss accumulators are per wave / per thread — so after the first tile
+    // (whose pre-split is ordered only by this barrier) the tile loop runs on two barriers
+    if (!(MLP2_BAR1_SKIP && PRE && NCB >= 4 && tile != (int)blockIdx.x)) bar_lds();
     STAMP(1);
     if (tile + gridDim.x < ntiles) {
       TileImg tn = ti;
