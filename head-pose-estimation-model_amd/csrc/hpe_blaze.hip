@@ -1236,6 +1236,9 @@ static bf_fn pick_direct(int s, int dw, int nc) {
 // The geometry is the BlazeFace backbone's (host-checked against the plan records).
 // ------------------------------------------------------------------------------------------------
 #define BFF_NW 8
+#ifndef BFF_SPLIT45
+#define BFF_SPLIT45 1   // w2 both block-1 chunks; w3 and w7 one output-channel chunk each of blocks 4 / 5
+#endif
 #ifdef BFF_STAMPS   // per-wave busy cycles (task time, barrier waits excluded) of workgroup 0
 #define BFF_BAR() do { bff_busy += __builtin_amdgcn_s_memtime() - bff_t0; bar_lds(); bff_t0 = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -1270,14 +1273,15 @@ struct BfFrontArgs {
 
 // pointwise weights of block K for this lane (output channel nc * 32 + l32, channel quads
 // c0 = 4 half + 8 k): the split_w pairs bf_rows_kernel keeps in LDS
-template <int K>
-__device__ __forceinline__ void bff_wload(const BfFrontArgs& a, f32x4 (&wr)[(BffL<K>::COUTP + 31) / 32][BffL<K>::CINP / 8],
-                                          float (&bias)[(BffL<K>::COUTP + 31) / 32], int l32, int half) {
+// (output-channel chunks NC0 .. NC0 + NCN - 1)
+template <int K, int NC0 = 0, int NCN = (BffL<K>::COUTP + 31) / 32>
+__device__ __forceinline__ void bff_wload(const BfFrontArgs& a, f32x4 (&wr)[NCN][BffL<K>::CINP / 8],
+                                          float (&bias)[NCN], int l32, int half) {
   using L = BffL<K>;
-  constexpr int NC = (L::COUTP + 31) / 32, NKS = L::CINP / 8;
+  constexpr int NKS = L::CINP / 8;
 #pragma unroll
-  for (int nc = 0; nc < NC; ++nc) {
-    const int n = nc * 32 + l32;
+  for (int nc = 0; nc < NCN; ++nc) {
+    const int n = (NC0 + nc) * 32 + l32;
 #pragma unroll
     for (int k = 0; k < NKS; ++k)
       wr[nc][k] = n < L::COUTP ? split_w(ld4(a.params + a.pww[K] + n * L::CINP + 4 * half + 8 * k)) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1297,14 +1301,16 @@ __device__ __forceinline__ void bff_dwload(const BfFrontArgs& a, f32x4 (&dwr)[Bf
 }
 
 // DWR: the depthwise table of the lane's channel quads in registers (dwr, bff_dwload) instead of
-// 10 ds_read_b128 per K-step from the LDS copy (the front is LDS-bandwidth-bound)
-template <int K, bool DWR = false>
+// 10 ds_read_b128 per K-step from the LDS copy (the front is LDS-bandwidth-bound).  NC0 / NC: the
+// output-channel chunks this wave computes (two waves may share a row, each with its own chunks:
+// the same depthwise, each chunk's products in the same order)
+template <int K, bool DWR = false, int NC0 = 0, int NC = (BffL<K>::COUTP + 31) / 32>
 __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
-                                          const f32x4 (&wr)[(BffL<K>::COUTP + 31) / 32][BffL<K>::CINP / 8],
-                                          const float (&bias)[(BffL<K>::COUTP + 31) / 32], float* gout, int l32, int half,
+                                          const f32x4 (&wr)[NC][BffL<K>::CINP / 8],
+                                          const float (&bias)[NC], float* gout, int l32, int half,
                                           const f32x4 (*dwr)[10] = nullptr) {
   using L = BffL<K>;
-  constexpr int NC = (L::COUTP + 31) / 32, NKS = L::CINP / 8, ROW = L::COLS * L::CS;
+  constexpr int NKS = L::CINP / 8, ROW = L::COLS * L::CS;
   f32x16 acc[NC];
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) acc[nc] = (f32x16){};
@@ -1346,7 +1352,7 @@ __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
   if (BFF_RESB && !zero) {
 #pragma unroll
     for (int nc = 0; nc < NC; ++nc) {
-      const int n = min(nc * 32 + l32, L::CINP - 1);  // n >= CINP: read a valid address, unused
+      const int n = min((NC0 + nc) * 32 + l32, L::CINP - 1);  // n >= CINP: read a valid address, unused
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int x = 32 * c + 4 * half + (g & 3) + 8 * (g >> 2);
@@ -1362,7 +1368,7 @@ __device__ __forceinline__ void bff_block(float* lds, int oy, int c, bool zero,
   }
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) {
-    const int n = nc * 32 + l32;
+    const int n = (NC0 + nc) * 32 + l32;
     if (n >= L::COUTP) continue;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -1491,7 +1497,7 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
         BFF_BAR();
       }
     }
-  } else if (wave < 4) {
+  } else if (wave == 2 || (wave == 3 && !BFF_SPLIT45)) {
     f32x4 wr[1][3], dwr[3][10];
     float bias[1];
     bff_wload<1>(a, wr, bias, l32, half);
@@ -1500,7 +1506,29 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
       frame_begin(img);
       for (int p = 0; p < BFF_PHASES; ++p) {
         const int oy = p - 2;
-        if (oy >= 0 && oy <= 64) bff_block<1, true>(lds, oy, wave - 2, oy == 64, wr, bias, nullptr, l32, half, dwr);
+        if (oy >= 0 && oy <= 64) {
+          bff_block<1, true>(lds, oy, wave - 2, oy == 64, wr, bias, nullptr, l32, half, dwr);
+          if (BFF_SPLIT45) bff_block<1, true>(lds, oy, 1, oy == 64, wr, bias, nullptr, l32, half, dwr);
+        }
+        BFF_BAR();
+      }
+    }
+  } else if (wave == 3) {
+    // blocks 4 / 5's second output-channel chunk (w7 has the first)
+    f32x4 w4[1][4], w5[1][5];
+    float b4[1], b5[1];
+    bff_wload<4, 1, 1>(a, w4, b4, l32, half);
+    bff_wload<5, 1, 1>(a, w5, b5, l32, half);
+    for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
+      frame_begin(img);
+      float* gout = a.dst + img * (32 * 32 * 48);
+      for (int p = 0; p < BFF_PHASES; ++p) {
+        if (p & 1) {
+          if (p >= 13) bff_block<5, false, 1, 1>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
+        } else {
+          const int oy = (p - 10) >> 1;
+          if (p >= 10 && oy <= 32) bff_block<4, false, 1, 1>(lds, oy, 0, oy == 32, w4, b4, nullptr, l32, half);
+        }
         BFF_BAR();
       }
     }
@@ -1558,19 +1586,20 @@ __global__ void __launch_bounds__(BFF_NW * 64) bf_front_kernel(BfFrontArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   } else {
-    f32x4 w4[2][4], w5[2][5];
-    float b4[2], b5[2];
-    bff_wload<4>(a, w4, b4, l32, half);
-    bff_wload<5>(a, w5, b5, l32, half);
+    constexpr int N45 = BFF_SPLIT45 ? 1 : 2;
+    f32x4 w4[N45][4], w5[N45][5];
+    float b4[N45], b5[N45];
+    bff_wload<4, 0, N45>(a, w4, b4, l32, half);
+    bff_wload<5, 0, N45>(a, w5, b5, l32, half);
     for (int64_t img = blockIdx.x; img < a.nimg; img += gridDim.x) {
       frame_begin(img);
       float* gout = a.dst + img * (32 * 32 * 48);
       for (int p = 0; p < BFF_PHASES; ++p) {
         if (p & 1) {
-          if (p >= 13) bff_block<5>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
+          if (p >= 13) bff_block<5, false, 0, N45>(lds, (p - 13) >> 1, 0, false, w5, b5, gout, l32, half);
         } else {
           const int oy = (p - 10) >> 1;
-          if (p >= 10 && oy <= 32) bff_block<4>(lds, oy, 0, oy == 32, w4, b4, nullptr, l32, half);
+          if (p >= 10 && oy <= 32) bff_block<4, false, 0, N45>(lds, oy, 0, oy == 32, w4, b4, nullptr, l32, half);
         }
         BFF_BAR();
       }
