@@ -160,6 +160,8 @@ def summarize_line(tag, line, steps=10, warmup=2, pmc_steps=5, pmc_warmup=1):
         tot_ns = sum(sum(v) for v in groups.values()) / nfwd
         fb = wb = 0.0
         for key, cs in ctr.items():
+            if key[0].startswith(('at::', '__amd_rocclr')):   # the bench's synthetic frames / copies
+                continue
             if 'FETCH_SIZE' in cs:
                 fb += 2 * 1024 * cs['FETCH_SIZE'][1] * cs['FETCH_SIZE'][0]
             if 'WRITE_SIZE' in cs:
@@ -167,7 +169,11 @@ def summarize_line(tag, line, steps=10, warmup=2, pmc_steps=5, pmc_warmup=1):
         res = {'kernel': 'all launches of one forward (bf_* + head GEMMs + regressor programs)',
                'avg_ns': tot_ns, 'forwards': nfwd, 'timed_region_only': True}
         if ctr:
-            res.update({'fetch_bytes': fb / nfwd, 'write_bytes': wb / nfwd, 'hbm_bytes_per_launch': (fb + wb) / nfwd})
+            # the PMC passes run their own step counts: their forwards are their own front dispatches
+            pf = [max(v[0] for v in cs.values()) for k, cs in ctr.items() if k[0].startswith(('bf_stem', 'bf_front'))]
+            npf = max(1, min(pf)) if pf else nfwd
+            res.update({'fetch_bytes': fb / npf, 'write_bytes': wb / npf, 'hbm_bytes_per_launch': (fb + wb) / npf,
+                        'pmc_forwards': npf})
         return res
     key = max(groups, key=lambda k: sum(groups[k]))
     d = groups[key]
