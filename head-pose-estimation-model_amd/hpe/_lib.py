@@ -59,7 +59,13 @@ SIGNATURES = {
     'hpe_set_exact_fp32': (ctypes.c_int, [ctypes.c_int]),
     'hpe_act_probe': (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int64, ctypes.c_void_p]),
+    'hpe_rccl_available': (ctypes.c_int, []),
+    'hpe_rccl_unique_id': (ctypes.c_int, [_vp]),
+    'hpe_rccl_comm_init': (ctypes.c_int, [_vp, _i32, _i32, ctypes.POINTER(_vp)]),
+    'hpe_rccl_comm_destroy': (ctypes.c_int, [_vp]),
+    'hpe_rccl_allreduce': (ctypes.c_int, [_vp, _i64, _vp, _vp]),
 }
+RCCL_ID_BYTES = 128   # HPE_RCCL_ID_BYTES
 
 _lib = None
 _CSRC = os.path.join(os.path.dirname(_HERE), 'csrc')

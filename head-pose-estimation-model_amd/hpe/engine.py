@@ -25,6 +25,51 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_RCCL_COMMS = {}   # (group, device) -> the library's RCCL communicator for hpe_fit_steps_dp
+
+
+def rccl_comm(mod, grp, device, nranks=None, rank=None):
+    """The library's own RCCL communicator over the ranks of process group `grp` (one per group and
+    device, made once: rank 0's hpe_rccl_unique_id broadcast over the group, then
+    hpe_rccl_comm_init on every rank's current device), or None when the group is not an nccl
+    (RCCL) group on a GPU, librccl does not load, or HPE_NATIVE_RCCL=0 — the caller then keeps
+    the torch.distributed hook.  nranks / rank default to the group's."""
+    if os.environ.get('HPE_NATIVE_RCCL', '1') == '0' or device is None or torch.device(device).type != 'cuda':
+        return None
+    if str(mod.get_backend(grp)).lower() != 'nccl':
+        return None
+    lib = _lib.load()
+    if not lib.hpe_rccl_available():
+        return None
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device('cuda', torch.cuda.current_device())
+    pg = grp if grp is not None else mod.group.WORLD   # the group object itself: a re-initialised
+    key = (pg, device.index)                           # default group gets its own communicator
+    if key not in _RCCL_COMMS:
+        nranks = mod.get_world_size(grp) if nranks is None else nranks
+        rank = mod.get_rank(grp) if rank is None else rank
+        uid = ctypes.create_string_buffer(_lib.RCCL_ID_BYTES)
+        if rank == 0:
+            _lib.check(lib.hpe_rccl_unique_id(uid), 'hpe_rccl_unique_id')
+        obj = [bytes(uid.raw) if rank == 0 else None]
+        mod.broadcast_object_list(obj, group=grp, group_src=0)
+        uid = ctypes.create_string_buffer(obj[0], _lib.RCCL_ID_BYTES)
+        comm = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _lib.check(lib.hpe_rccl_comm_init(uid, int(nranks), int(rank), ctypes.byref(comm)), 'hpe_rccl_comm_init')
+        _RCCL_COMMS[key] = comm
+    return _RCCL_COMMS[key]
+
+
+def release_rccl_comms():
+    """Destroy every communicator rccl_comm made (before its process group is destroyed)."""
+    lib = _lib.load()
+    while _RCCL_COMMS:
+        _, comm = _RCCL_COMMS.popitem()
+        _lib.check(lib.hpe_rccl_comm_destroy(comm), 'hpe_rccl_comm_destroy')
+
+
 class _Compiled:
     def __init__(self, prog):
         self.prog = prog
@@ -218,7 +263,8 @@ class Engine:
     def optim_grid(self):
         return _lib.load().hpe_optim_grid(self.n_train)
 
-    # the all-reduce hook hpe_fit_steps_dp calls once per step (int (*)(float*, int64, void*, void*))
+    # the all-reduce hook hpe_fit_steps_dp calls once per step (int (*)(float*, int64, void*, void*)):
+    # hpe_rccl_allreduce on GPU ranks of an nccl (RCCL) group, else this Python callback
     ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p)
 
     def fit_steps(self, opt, x, y, perm, batch, stats, seed_base, x_bound=0.0, P=1, dist=None):
@@ -239,18 +285,22 @@ class Engine:
         n = int(perm.numel())
         steps = (n + batch - 1) // batch
         ws = c.workspace(min(batch, n) * P, self.device)
-        if dist is not None and dist[0].get_world_size(dist[1]) > 1:
+        if dist is not None and (dist[0].get_world_size(dist[1]) > 1 or os.environ.get('HPE_FIT_DP_ONE_RANK') == '1'):
             mod, grp = dist
             errors = []
-
-            def allreduce(_buf, _n, _stream, _user):
-                try:
-                    mod.all_reduce(self.grad, group=grp)
-                    return 0
-                except Exception as e:   # surfaces as HPE_ERUNTIME from the C loop, re-raised below
-                    errors.append(e)
-                    return 1
-            hook = self.ALLREDUCE_FN(allreduce)
+            comm = rccl_comm(mod, grp, self.device)
+            if comm is not None:
+                # GPU ranks: the library's own RCCL sum on the step's stream, no Python per step
+                hook, user = ctypes.cast(lib.hpe_rccl_allreduce, ctypes.c_void_p), comm
+            else:
+                def allreduce(_buf, _n, _stream, _user):
+                    try:
+                        mod.all_reduce(self.grad, group=grp)
+                        return 0
+                    except Exception as e:   # surfaces as HPE_ERUNTIME from the C loop, re-raised below
+                        errors.append(e)
+                        return 1
+                hook, user = self.ALLREDUCE_FN(allreduce), None
             done = ctypes.c_int64(0)
             rc = lib.hpe_fit_steps_dp(c.h, _ptr(self.params), _ptr(self.params_t), _ptr(self.m), _ptr(self.v),
                                       _ptr(self.l2), _ptr(self.tpos), self.n_train, _ptr(x), _ptr(y), _ptr(perm),
@@ -259,7 +309,7 @@ class Engine:
                                       int(seed_base) & 0xFFFFFFFFFFFFFFFF, int(self.iterations), _ptr(ws),
                                       _ptr(self.grad), _ptr(stats), int(stats.shape[1]),
                                       mod.get_rank(grp), mod.get_world_size(grp),
-                                      ctypes.cast(hook, ctypes.c_void_p), None, ctypes.byref(done), _stream())
+                                      ctypes.cast(hook, ctypes.c_void_p), user, ctypes.byref(done), _stream())
             # the steps whose optimizer update was applied advance the iteration count even when
             # the epoch stopped early (Adam's bias correction and the dropout seeds of a retry stay
             # in step with params / m / v)

@@ -285,8 +285,10 @@ class Model:
             # without a Python round trip per step); HPE_FIT_STEPS=0 keeps the Python loop
             c_steps = not fused and os.environ.get('HPE_FIT_STEPS', '1') != '0'
             if c_steps:
+                # (HPE_FIT_DP_ONE_RANK=1: the data-parallel step loop on a one-rank group, for tests)
+                dp = world > 1 or os.environ.get('HPE_FIT_DP_ONE_RANK') == '1'
                 eng.fit_steps(self.optimizer, xd, yd, idx, bs, stats, hrandom.dropout_seed(0), x_bound, P,
-                              dist=self._dist if world > 1 else None)
+                              dist=self._dist if dp else None)
             for s in range(0 if fused or c_steps else steps):
                 b0, b1 = s * bs, min(n, (s + 1) * bs)
                 nb = b1 - b0

@@ -149,6 +149,19 @@ int hpe_fit_steps_dp(const hpe_program *prog, float *params, float *params_t, fl
                      int32_t stats_stride, int32_t rank, int32_t world, hpe_allreduce_fn allreduce,
                      void *user, int64_t *steps_done, void *stream);
 
+/* Native RCCL all-reduce for hpe_fit_steps_dp on GPU ranks (csrc/hpe_rccl.hip; librccl opened at
+ * run time): replaces the caller's per-step hook (e.g. a torch.distributed callback, one
+ * interpreter re-entry per step) by an RCCL sum enqueued on the step's own stream.  Rank 0 calls
+ * hpe_rccl_unique_id, the caller broadcasts the HPE_RCCL_ID_BYTES bytes to every rank, each rank
+ * calls hpe_rccl_comm_init on its current device; then hpe_fit_steps_dp(..., allreduce =
+ * hpe_rccl_allreduce, user = the communicator, ...).  hpe_rccl_available: 1 when librccl loads. */
+#define HPE_RCCL_ID_BYTES 128
+int hpe_rccl_available(void);
+int hpe_rccl_unique_id(void *id_out);
+int hpe_rccl_comm_init(const void *id, int32_t nranks, int32_t rank, void **comm_out);
+int hpe_rccl_comm_destroy(void *comm);
+int hpe_rccl_allreduce(float *buf, int64_t n, void *stream, void *comm);
+
 /* ---------------------------------------------------------------------------------------------
  * One whole epoch of model.fit in ONE launch (csrc/hpe_fit.hip) — replaces the per-step loop of
  * Keras fit (train_96.py:175-183, train_88.py:355-363) for the reference's own regime: 1x1 maps

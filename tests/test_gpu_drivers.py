@@ -168,3 +168,70 @@ def test_bench_run_train_two_ranks_matches_one(tmp_path):
     assert float(dp['mse']) == pytest.approx(mse, rel=1e-4)
     for k, v in m.weights_dict().items():
         np.testing.assert_allclose(dp[k.replace('/', '|')], v, rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+def _rccl_worker(rank, port, out):
+    for p in (ROOT, PKG, os.path.dirname(os.path.abspath(__file__))):
+        sys.path.insert(0, p)
+    import ctypes
+    import torch.distributed as dist
+    import hpe as H
+    from hpe import _lib
+    from hpe import engine as E
+    from hpe import keras as kk
+    from util import features as f_, fixture as fx, labels as lb
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    lib = _lib.load()
+    # the library's own communicator over the group's one rank: its sum is the identity
+    comm = E.rccl_comm(dist, None, dev)
+    buf = torch.randn(1001, device=dev)
+    ref = buf.clone()
+    rc = lib.hpe_rccl_allreduce(ctypes.c_void_p(buf.data_ptr()), buf.numel(),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), comm)
+    torch.cuda.synchronize()
+    identity = comm is not None and rc == 0 and torch.equal(buf, ref)
+    # the data-parallel step loop (hpe_fit_steps_dp) on the one-rank group: the native RCCL hook
+    # against the torch.distributed hook, and against the single-rank step loop
+    mc, w = fx('sqnu665j')
+    os.environ['HPE_FIT_FUSED'] = '0'
+    res = {}
+    for mode in ('native', 'torch', 'single'):
+        os.environ['HPE_NATIVE_RCCL'] = '1' if mode == 'native' else '0'
+        os.environ['HPE_FIT_DP_ONE_RANK'] = '0' if mode == 'single' else '1'
+        H.set_seed(3)
+        m = H.model_from_config(mc, w).distribute()
+        m.compile(optimizer=kk.optimizers.Adam(learning_rate=1e-3), loss='mse', metrics=['mae'])
+        h = m.fit(f_(160, 96, seed=21), lb(160, seed=22), batch_size=64, epochs=2, shuffle=True, verbose=0)
+        res[mode] = (np.asarray(h.history['loss']), m.weights_dict())
+    same = all(np.array_equal(res['native'][1][k], v) for k, v in res['torch'][1].items())
+    same = same and np.array_equal(res['native'][0], res['torch'][0])
+    ncomm = len(E._RCCL_COMMS)
+    E.release_rccl_comms()
+    dist.destroy_process_group()
+    np.savez(out, identity=identity, same=same, ncomm=ncomm, loss=res['native'][0], loss1=res['single'][0],
+             **{'n|' + k.replace('/', '|'): v for k, v in res['native'][1].items()},
+             **{'s|' + k.replace('/', '|'): v for k, v in res['single'][1].items()})
+
+
+def test_native_rccl_allreduce_one_rank(tmp_path):
+    """hpe_fit_steps_dp with the library's own RCCL all-reduce as its per-step
+    hook (hpe_rccl_allreduce, enqueued on the step's stream; no Python per step) on an nccl group of
+    ONE rank — the one RCCL configuration a one-GPU box can run: the communicator is made (id
+    broadcast over the group), its sum is the identity, and the native hook gives the torch.distributed
+    hook's weights bit for bit (and the single-rank loop's within float tolerance).  Across GPUs it is
+    unexercised until an 8-GPU run."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / 'rccl.npz')
+    mp.spawn(_rccl_worker, args=(_free_port(), out), nprocs=1, join=True)
+    r = np.load(out)
+    assert bool(r['identity'])
+    assert int(r['ncomm']) == 1          # the native hook was the one used
+    assert bool(r['same'])
+    np.testing.assert_allclose(r['loss'], r['loss1'], rtol=1e-5)
+    for k in r.files:
+        if k.startswith('n|'):
+            np.testing.assert_allclose(r[k], r['s|' + k[2:]], rtol=1e-4, atol=1e-6, err_msg=k)
