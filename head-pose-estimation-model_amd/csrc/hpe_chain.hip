@@ -18,10 +18,14 @@
 #define CHAIN_NW 12                     // waves per workgroup (3 per SIMD)
 #define CHAIN_KH 48                     // rows of 24 16-B chunks: 88- or 96-channel inputs
 #define CHAIN_XF (32 * CHAIN_KH * 2)    // floats per wave X tile
-#define CHAIN_TAB 1280                  // floats of shared weight tables per workgroup
+#define CHAIN_QTAB 384                  // ints of chain_split_kernel's source-offset table (at the end of the tables)
+#define CHAIN_TAB (1280 + CHAIN_QTAB)   // floats of shared weight tables per workgroup
 // cache policy of the X stream's LDS-DMA (read once): non-temporal (aux 2).  The access pattern
 // alone (scripts/stream_probe.hip: 12 waves x one 12-KiB tile in flight, MI355X) streams at
 // 7.0 TB/s nt vs 6.1 TB/s with the default policy
+#ifndef CHAIN_FASTISSUE
+#define CHAIN_FASTISSUE 1   // full non-gather tiles: per-lane source offsets set once (0: recomputed per piece)
+#endif
 #ifndef CHAIN_AUX
 #define CHAIN_AUX 2
 #endif
@@ -243,14 +247,34 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
   const int64_t gw = (int64_t)blockIdx.x * CHAIN_SNW + wave;
   const int64_t nw = (int64_t)gridDim.x * CHAIN_SNW;
   // HBM -> LDS slot d: 12 x 1 KiB global_load_lds, swizzled source chunks, rows past the end repeat
-  // the last row; per-lane (row, chunk) recomputed per tile from an opaque lane id (cheap VALU)
+  // the last row; per-lane (row, chunk) recomputed per tile from an opaque lane id (cheap VALU).
+  // Full tiles without a gather (CHAIN_FASTISSUE, round 6): piece pc = 3 q + t holds row r_t + 8 q
+  // and chunk c_t ^ (4 (q & 1)) of lane's slot (64 pc = 8 rows of 24 chunks per 3 pieces; +8 rows
+  // flips bit 2 of the swizzle), so each lane's 12 source offsets are 3 pairs of per-lane values
+  // (qo[t][q & 1], 6 VGPRs set once) plus the wave-uniform 8 q Cin: one address add per piece
+  // instead of ~15 VALU of division / swizzle / clamp / 64-bit address math (the issue was ~180 of
+  // the loop's ~800 VALU per tile, and the kernel runs near the VALU issue limit at 3 waves per SIMD)
+  // (the 6 x 64 offsets live in an LDS table, qtab[(2 t + e) * 64 + lane], written by wave 0 before
+  // the prologue's barrier and read at each issue: 6 resident VGPRs spilled the kernel)
+  int* qtab = (int*)(lds + CHAIN_TAB - CHAIN_QTAB);
   auto issue = [&](int64_t tile, int d) {
     const int64_t row0 = tile * 32;
+    float* xs = ring + d * CHAIN_XF;
+    if (CHAIN_FASTISSUE && !GATHER && row0 + 32 <= nrows) {
+      const float* xt = args.x + row0 * Cin;
+      int qo[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) qo[i] = qtab[i * 64 + lane];
+#pragma unroll
+      for (int pc = 0; pc < 12; ++pc)
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(xt + (pc / 3) * 8 * Cin + qo[2 * (pc % 3) + ((pc / 3) & 1)]),
+                                         (lds_ptr_t)(xs + pc * 256), 16, 0, CHAIN_AUX);
+      return;
+    }
     int lz = lane;
     asm volatile("" : "+v"(lz));
     const int last = (int)min<int64_t>(nrows - 1 - row0, 31);
     const float* xt = args.x + row0 * Cin;
-    float* xs = ring + d * CHAIN_XF;
 #pragma unroll
     for (int pc = 0; pc < 12; ++pc) {
       const int slot = pc * 64 + lz;
@@ -269,6 +293,15 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + pc * 256), 16, 0, CHAIN_AUX);
     }
   };
+  if (CHAIN_FASTISSUE && !GATHER && threadIdx.x < 192) {
+    const int t = threadIdx.x >> 6, slot = t * 64 + lane, r = slot / 24, ph = slot - r * 24;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = csw(r, ph) ^ (4 * e);
+      qtab[(2 * t + e) * 64 + lane] = r * Cin + 4 * (4 * c < Cin ? c : 0);
+    }
+  }
+  __syncthreads();
   // the ring's first tiles go out before the weight prologue
 #pragma unroll
   for (int d = 0; d < CHAIN_SD; ++d)
