@@ -77,3 +77,20 @@ def test_fused_kernel_programs_pass_host_validation():
     h = ctypes.c_void_p()
     rc = lib.hpe_program_create(w.ctypes.data_as(ctypes.c_void_p), w.size, ctypes.byref(h))
     assert rc != 1, lib.hpe_last_error()
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason='libhpe.so not built')
+def test_rccl_hook_argument_checks_without_gpu():
+    """hpe_rccl_*: argument errors come back as HPE_EINVAL with a message, before any RCCL or
+    device call (the hook itself runs in tests/test_gpu_drivers.py on a one-rank nccl group)."""
+    lib = _lib.load()
+    assert lib.hpe_rccl_available() in (0, 1)
+    assert lib.hpe_rccl_allreduce(None, 16, None, None) == 1
+    assert b'hpe_rccl_allreduce' in lib.hpe_last_error()
+    comm = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(_lib.RCCL_ID_BYTES)
+    assert lib.hpe_rccl_comm_init(uid, 0, 0, ctypes.byref(comm)) == 1
+    assert lib.hpe_rccl_comm_init(uid, 2, 2, ctypes.byref(comm)) == 1 and not comm.value
+    assert lib.hpe_rccl_comm_init(None, 1, 0, ctypes.byref(comm)) == 1
+    assert lib.hpe_rccl_unique_id(None) == 1
+    assert lib.hpe_rccl_comm_destroy(None) == 0
