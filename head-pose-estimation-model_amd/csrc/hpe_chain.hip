@@ -23,6 +23,9 @@
 // cache policy of the X stream's LDS-DMA (read once): non-temporal (aux 2).  The access pattern
 // alone (scripts/stream_probe.hip: 12 waves x one 12-KiB tile in flight, MI355X) streams at
 // 7.0 TB/s nt vs 6.1 TB/s with the default policy
+#ifndef CHAIN_HALF2
+#define CHAIN_HALF2 1   // F2 <= 16: layer 2's padding registers skipped (0: all 16 per lane)
+#endif
 #ifndef CHAIN_FASTISSUE
 #define CHAIN_FASTISSUE 1   // full non-gather tiles: per-lane source offsets set once (0: recomputed per piece)
 #endif
@@ -433,17 +436,31 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
                         acc2);
       }
       chk += sum16(acc2);
+      // layer 2's unit of register g is (g & 3) + 8 (g >> 2) + 4 h: with F2 <= 16 (hrchr82r's 16)
+      // registers 8..15 hold only padding units (zero weights, zero bias, zero head weights), so
+      // their activations and head terms (+0 each) are skipped: 8 of 16 tanh per lane and tile
+      // (CHAIN_HALF2, round 6)
+      if (CHAIN_HALF2 && F2 <= 16) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
-        acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
+        for (int g = 0; g < 8; ++g) {
+          const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
+          acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
+          acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
+        }
       }
       h = acc2;
     }
     bad |= !(fabsf(chk) <= 3.0e38f);
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    const int ng = (CHAIN_HALF2 && F2 > 0 && F2 <= 16) ? 8 : 16;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
+      if (g >= ng) break;
       const int nn = (g & 3) + 8 * (g >> 2) + 4 * half;
       const f32x4 w = *(const f32x4*)(tw3 + toff + nn * 4);
       s0 = fmaf(h[g], w.x, s0);
