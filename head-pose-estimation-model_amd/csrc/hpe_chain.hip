@@ -23,6 +23,12 @@
 // cache policy of the X stream's LDS-DMA (read once): non-temporal (aux 2).  The access pattern
 // alone (scripts/stream_probe.hip: 12 waves x one 12-KiB tile in flight, MI355X) streams at
 // 7.0 TB/s nt vs 6.1 TB/s with the default policy
+#ifndef CHAIN_EXACT_RING
+#define CHAIN_EXACT_RING 1     // the exact-fp32 path on chain_split_kernel's streaming (0: chain_fwd_kernel)
+#endif
+#ifndef CHAIN_EXACT_DEFAULT
+#define CHAIN_EXACT_DEFAULT 0  // 1: every launch on the exact ring kernel (no split, no guard)
+#endif
 #ifndef CHAIN_HALF2
 #define CHAIN_HALF2 1   // F2 <= 16: layer 2's padding registers skipped (0: all 16 per lane)
 #endif
@@ -228,7 +234,11 @@ __global__ void __launch_bounds__(CHAIN_NW * 64) chain_fwd_kernel(Args args) {
 // work cut 5x the kernel is bound by the X stream alone.  A tile whose accumulators come out
 // non-finite (an input or activation outside the fp16 range) sets the guard word; the exact-fp32
 // kernel launched behind it then recomputes the whole launch.
-template <int A1, int A2, int A3, int GATHER>
+// EX (round 6): the same streaming structure with chain_fwd_kernel's exact fp32 MFMAs
+// (v_mfma_f32_32x32x2_f32, 64 per tile, no data-side split): 4,096 MFMA cycles per tile against the
+// split path's ~2.6 k cycles of VALU issue per wave-tile (the split's data side is 224 VALU per
+// tile); same products, order and results as chain_fwd_kernel, no overflow guard needed
+template <int A1, int A2, int A3, int GATHER, bool EX = false>
 __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int* prog = args.prog;
@@ -326,9 +336,17 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
   // A of layer 1: W1^T[n = l32][k], K-step s holds k = 16 s + 8 half + j (j = 0..7)
   // weight-side exponents (pow2_scale, hpe_common.h): W1 and W2 each enter their MFMAs scaled by
   // one power of two (their max |w| in [2^13, 2^14)); layer outputs come out as acc * inv
-  SplitW w1[6];
-  float inv1, inv2;
-  {
+  SplitW w1[EX ? 1 : 6];
+  float w1x[EX ? CHAIN_KH : 1];   // EX: W1 column n = l32 as the A operand, k = half * 48 + m
+  float inv1 = 1.f, inv2 = 1.f;
+  if constexpr (EX) {
+#pragma unroll
+    for (int m = 0; m < CHAIN_KH; ++m) {
+      const int k = half * CHAIN_KH + m;
+      const float v = P_[o[O_W] + (size_t)min(k, Cin - 1) * F1 + min(l32, F1 - 1)];
+      w1x[m] = (k < Cin && l32 < F1) ? v : 0.f;
+    }
+  } else {
     f32x8 v[6];
     float mx = 0.f;
 #pragma unroll
@@ -347,10 +365,15 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
     for (int s = 0; s < 6; ++s) w1[s] = split_w8(v[s] * sc);
   }
   __syncthreads();
+  float w2x[EX ? 16 : 1];   // EX: A of layer 2, W2^T[i = m = l32][k <-> hidden unit of register g]
+  if constexpr (EX) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) w2x[g] = tw2[((g & 3) + 8 * (g >> 2) + 4 * half) * 32 + l32];
+  }
   // A of layer 2: W2^T[m = l32][n], in the k order of an accumulator used as the B operand:
   // element j of K-step s of lane half h <-> hidden unit 16 s + 8 (j >> 2) + 4 h + (j & 3)
-  SplitW w2[2];
-  {
+  SplitW w2[EX ? 1 : 2];
+  if constexpr (!EX) {
     f32x8 v[2];
     float mx = 0.f;
 #pragma unroll
@@ -407,12 +430,23 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
     const float* xr = xs + l32 * 96;
     const int sw = (l32 >> 1) & 7;
     f32x16 acc = {};
+    if constexpr (EX) {
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int c0 = 4 * s + 2 * half;
-      const f32x4 a0 = *(const f32x4*)(xr + 4 * (c0 ^ sw));
-      const f32x4 a1 = *(const f32x4*)(xr + 4 * ((c0 + 1) ^ sw));
-      acc = mfma3_wd(w1[s], split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), acc);
+      for (int m = 0; m < CHAIN_KH; m += 4) {
+        const f32x4 a = *(const f32x4*)(xr + 4 * ((half * 12 + m / 4) ^ sw));
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1x[m + 0], a.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1x[m + 1], a.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1x[m + 2], a.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1x[m + 3], a.w, acc, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const int c0 = 4 * s + 2 * half;
+        const f32x4 a0 = *(const f32x4*)(xr + 4 * (c0 ^ sw));
+        const f32x4 a1 = *(const f32x4*)(xr + 4 * ((c0 + 1) ^ sw));
+        acc = mfma3_wd(w1[s], split_d8(f32x8{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}), acc);
+      }
     }
     // the slot's reads are consumed by the MFMAs above: the previous tile's outputs go out, then
     // the tile CHAIN_SD ahead streams into this slot during the rest of this tile's arithmetic
@@ -420,22 +454,27 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
     asm volatile("" ::: "memory");
     if (k > 0) store_prev();
     if (tile + CHAIN_SD * nw < ntiles) issue(tile + CHAIN_SD * nw, d);
-    float chk = sum16(acc);
+    float chk = EX ? 0.f : sum16(acc);
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, fmaf(acc[g], inv1, b1r[g]));
+    for (int g = 0; g < 16; ++g) acc[g] = cact<A1>(act1, EX ? acc[g] + b1r[g] : fmaf(acc[g], inv1, b1r[g]));
     int toff = 0;
     asm volatile("" : "+v"(toff));
     // ---- layer 2 (optional): B = A1^T straight from the accumulator registers 8 s .. 8 s + 7 ----
     f32x16 h = acc;
     if (F2 > 0) {
       f32x16 acc2 = {};
+      if constexpr (EX) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        acc2 = mfma3_wd(w2[s], split_d8(f32x8{acc[8 * s + 0], acc[8 * s + 1], acc[8 * s + 2], acc[8 * s + 3],
-                                              acc[8 * s + 4], acc[8 * s + 5], acc[8 * s + 6], acc[8 * s + 7]}),
-                        acc2);
+        for (int g = 0; g < 16; ++g) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2x[g], acc[g], acc2, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          acc2 = mfma3_wd(w2[s], split_d8(f32x8{acc[8 * s + 0], acc[8 * s + 1], acc[8 * s + 2], acc[8 * s + 3],
+                                                acc[8 * s + 4], acc[8 * s + 5], acc[8 * s + 6], acc[8 * s + 7]}),
+                          acc2);
+        }
+        chk += sum16(acc2);
       }
-      chk += sum16(acc2);
       // layer 2's unit of register g is (g & 3) + 8 (g >> 2) + 4 h: with F2 <= 16 (hrchr82r's 16)
       // registers 8..15 hold only padding units (zero weights, zero bias, zero head weights), so
       // their activations and head terms (+0 each) are skipped: 8 of 16 tanh per lane and tile
@@ -444,13 +483,13 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
           const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
-          acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
+          acc2[g] = cact<A2>(act2, EX ? acc2[g] + tb2[toff + mm] : fmaf(acc2[g], inv2, tb2[toff + mm]));
         }
       } else {
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int mm = (g & 3) + 8 * (g >> 2) + 4 * half;
-          acc2[g] = cact<A2>(act2, fmaf(acc2[g], inv2, tb2[toff + mm]));
+          acc2[g] = cact<A2>(act2, EX ? acc2[g] + tb2[toff + mm] : fmaf(acc2[g], inv2, tb2[toff + mm]));
         }
       }
       h = acc2;
@@ -478,7 +517,7 @@ __global__ void __launch_bounds__(CHAIN_SNW * 64) chain_split_kernel(Args args) 
     pv2 = cact<A3>(act3, s2 + tb3[2]);
   }
   if (gw < ntiles) store_prev();
-  if (bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!EX && bad) __hip_atomic_store(args.guard, args.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 typedef void (*chain_fn)(Args);
@@ -498,6 +537,8 @@ template <int A1, int A2, int A3, int G>
 struct ChainExact { static constexpr chain_fn f = chain_fwd_kernel<A1, A2, A3, G>; };
 template <int A1, int A2, int A3, int G>
 struct ChainSplit { static constexpr chain_fn f = chain_split_kernel<A1, A2, A3, G>; };
+template <int A1, int A2, int A3, int G>
+struct ChainExactRing { static constexpr chain_fn f = chain_split_kernel<A1, A2, A3, G, true>; };
 
 template <template <int, int, int, int> class K>
 static chain_fn pick(const int* o, bool gather) {
@@ -518,11 +559,12 @@ static int launch_one(chain_fn k, const Args& a, int grid, hipStream_t s, bool s
 int chain_launch(const int* w, const Args& a, int grid, hipStream_t s) {
   const int* o = w + w[H_OPS_OFF];
   const bool g = a.idx != nullptr;
-  if (hpe_exact_fp32() || !a.guard) {
+  if (CHAIN_EXACT_DEFAULT || hpe_exact_fp32() || !a.guard) {
     Args e = a;
     e.guard = nullptr;
     const int tv = hpe_tev_begin(s);
-    const int rc = launch_one(pick<ChainExact>(o, g), e, grid, s);
+    const int rc = CHAIN_EXACT_RING ? launch_one(pick<ChainExactRing>(o, g), e, grid, s, true)
+                                    : launch_one(pick<ChainExact>(o, g), e, grid, s);
     hpe_tev_end(s, tv);
     return rc;
   }
