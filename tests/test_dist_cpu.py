@@ -80,3 +80,31 @@ def test_two_rank_gradient_equals_single(tmp_path):
                 inv_count=1.0 / (37 * 3), seed=5)
     g1 = np.concatenate([r['grad'], [r['sse'], r['sae']]])
     np.testing.assert_allclose(g2, g1, rtol=1e-10, atol=1e-12)
+
+
+def _rccl_gate_worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), 'head-pose-estimation-model_amd'), here):
+        sys.path.insert(0, p)
+    from hpe import engine as E
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    # gloo group (or no GPU device): the native RCCL hook is not used, the torch.distributed
+    # callback stays; nothing is created (no device touched)
+    res = [E.rccl_comm(dist, None, torch.device('cuda', 0)) is None,
+           E.rccl_comm(dist, None, None) is None,
+           E.rccl_comm(dist, None, torch.device('cpu')) is None,
+           len(E._RCCL_COMMS) == 0]
+    if rank == 0:
+        torch.save(torch.tensor(res), out)
+    dist.destroy_process_group()
+
+
+def test_native_rccl_hook_gated_to_nccl_groups(tmp_path):
+    """hpe.engine.rccl_comm: the library's RCCL communicator is made only for nccl (RCCL) groups on
+    a GPU device; gloo ranks keep the torch.distributed per-step hook (two gloo ranks on CPU)."""
+    out = str(tmp_path / 'gate.pt')
+    mp.spawn(_rccl_gate_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert bool(torch.load(out, weights_only=True).all())
